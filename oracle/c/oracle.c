@@ -1,0 +1,1223 @@
+/* ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.h). Reference-faithful C CPU prover.
+ *
+ * Restates, function by function, with the SAME algorithm classes as the reference
+ * (this is the reported CPU baseline, SURVEY §8(d) / BASELINE.md):
+ *   eq_extension as log_n separate tables ........ /root/reference/src/data_structures/eq.rs:5-20
+ *   sum_over_y (row SpMV) ......................... r1cs_reader.rs:75-85
+ *   eval_on_x (hash-map sparse partial eval) ...... r1cs_reader.rs:91-117 (+ SparseMLExtensionMap [upstream])
+ *   sumcheck: every product of every multiplicand at t = 0..=max_multiplicands
+ *             (AHPForMLSumcheck::prove_round [upstream]) ... ahp/prover.rs:163-266
+ *   VariableBaseMSM (unsigned windows c = ln(N)+2, 2^c-1 buckets) [upstream ark-ec]
+ *   mKZG keygen / commit / open with duplicated scalars ... commitment/setup.rs:27-105,
+ *                                                        commit.rs:17-29, open.rs:19-58
+ *   FS argument + Blake2s512Rng transcript ........ lib.rs:58-146 (conventions: oracle/py/transcript.py)
+ * Single-threaded, like the reference as configured (Cargo.toml:10-27).
+ */
+#include "oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "blake2s.h"
+#include "curve.h"
+
+static __thread char g_err[256];
+static void set_err(const char *m) { snprintf(g_err, sizeof g_err, "%s", m); }
+const char *orc_last_error(void) { return g_err; }
+
+/* ============================================================== PRNG / generators */
+typedef struct { uint64_t s; } sm64;
+static uint64_t sm64_next(sm64 *r) {
+    r->s += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = r->s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+/* canonical Fr from 4 draws (top limb masked to 63 bits, reject >= r) */
+static void sm64_fr(sm64 *r, fr_t *out) {
+    for (;;) {
+        uint64_t c[4];
+        c[0] = sm64_next(r);
+        c[1] = sm64_next(r);
+        c[2] = sm64_next(r);
+        c[3] = sm64_next(r) & 0x7FFFFFFFFFFFFFFFULL;
+        if (!fr_geq_p(c)) {
+            fr_from_canon(out, c);
+            return;
+        }
+    }
+}
+static void sm64_fr_nonzero(sm64 *r, fr_t *out) {
+    do sm64_fr(r, out);
+    while (fr_is_zero(out));
+}
+
+typedef struct {
+    uint64_t *row_ptr;
+    uint32_t *col;
+    fr_t *val;
+    uint64_t nnz, cap;
+} mat_t;
+
+struct orc_inst {
+    int log_n, log_v;
+    uint64_t n;
+    mat_t m[3];
+    fr_t *z;
+};
+
+static void mat_init(mat_t *M, uint64_t n, uint64_t cap) {
+    M->row_ptr = (uint64_t *)calloc(n + 1, 8);
+    M->cap = cap ? cap : 1;
+    M->col = (uint32_t *)malloc(4 * M->cap);
+    M->val = (fr_t *)malloc(sizeof(fr_t) * M->cap);
+    M->nnz = 0;
+}
+static void mat_push(mat_t *M, uint32_t col, const fr_t *v) {
+    if (M->nnz == M->cap) {
+        M->cap *= 2;
+        M->col = (uint32_t *)realloc(M->col, 4 * M->cap);
+        M->val = (fr_t *)realloc(M->val, sizeof(fr_t) * M->cap);
+    }
+    M->col[M->nnz] = col;
+    M->val[M->nnz] = *v;
+    M->nnz++;
+}
+
+static void gen_uniform_3n(orc_inst *I, uint64_t seed) {
+    uint64_t n = I->n, mask = n - 1;
+    sm64 r = {seed};
+    fr_one(&I->z[0]);
+    for (uint64_t i = 1; i < n; ++i) sm64_fr_nonzero(&r, &I->z[i]);
+    for (int k = 0; k < 3; ++k) mat_init(&I->m[k], n, n);
+    for (uint64_t x = 0; x < n; ++x) {
+        fr_t al, be, ga, t, zi;
+        uint64_t a = sm64_next(&r) & mask;
+        sm64_fr(&r, &al);
+        uint64_t b = sm64_next(&r) & mask;
+        sm64_fr(&r, &be);
+        uint64_t c = sm64_next(&r) & mask;
+        fr_mul(&t, &al, &I->z[a]);
+        fr_mul(&t, &t, &be);
+        fr_mul(&t, &t, &I->z[b]);
+        fr_inv(&zi, &I->z[c]);
+        fr_mul(&ga, &t, &zi);
+        mat_push(&I->m[0], (uint32_t)a, &al);
+        mat_push(&I->m[1], (uint32_t)b, &be);
+        mat_push(&I->m[2], (uint32_t)c, &ga);
+        I->m[0].row_ptr[x + 1] = I->m[0].nnz;
+        I->m[1].row_ptr[x + 1] = I->m[1].nnz;
+        I->m[2].row_ptr[x + 1] = I->m[2].nnz;
+    }
+}
+
+/* ---- ref-shaped: TestSynthesizer (constraints.rs:39-110) + make_matrices_square ---- */
+typedef struct { uint64_t var; fr_t val; } assign_t; /* var = column index */
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+/* push a compactified row: sort columns, merge duplicates (coefficient = multiplicity) */
+static void push_lc_row(mat_t *M, uint64_t *cols, size_t k, uint64_t x) {
+    qsort(cols, k, 8, cmp_u64);
+    for (size_t i = 0; i < k;) {
+        size_t j = i;
+        while (j < k && cols[j] == cols[i]) ++j;
+        fr_t c;
+        fr_from_u64(&c, (uint64_t)(j - i));
+        if (!fr_is_zero(&c)) mat_push(M, (uint32_t)cols[i], &c);
+        i = j;
+    }
+    M->row_ptr[x + 1] = M->nnz;
+}
+
+static void gen_ref_shaped(orc_inst *I, uint64_t seed, int density) {
+    uint64_t n = I->n;
+    uint64_t num_public = 1ULL << I->log_v, num_private = n - num_public;
+    sm64 r = {seed};
+    /* column of instance var k = k; witness var j = num_public + j */
+    assign_t *as = (assign_t *)malloc(sizeof(assign_t) * (n + 4));
+    size_t nas = 0;
+    fr_t a_val, b_val;
+    uint64_t a_var, b_var;
+    uint64_t ninst = 1, nwit = 0;
+    fr_one(&I->z[0]);
+    sm64_fr(&r, &a_val);
+    a_var = ninst++;
+    I->z[a_var] = a_val;
+    as[nas].var = a_var, as[nas].val = a_val, nas++;
+    sm64_fr(&r, &b_val);
+    b_var = ninst++;
+    I->z[b_var] = b_val;
+    as[nas].var = a_var, as[nas].val = a_val, nas++; /* sic constraints.rs:47 */
+    for (uint64_t i = 0; i + 3 < num_public; ++i) {
+        fr_t v;
+        sm64_fr(&r, &v);
+        uint64_t var = ninst++;
+        I->z[var] = v;
+        as[nas].var = var, as[nas].val = v, nas++;
+    }
+    for (int k = 0; k < 3; ++k) mat_init(&I->m[k], n, 4 * n);
+    uint64_t num_sparse = (num_private - 1) * (uint64_t)(510 - density) / 510;
+    uint64_t x = 0;
+    uint64_t cols[3];
+    for (uint64_t i = 0; i < num_sparse; ++i, ++x) {
+        uint64_t off_idx = 2 + sm64_next(&r) % (num_public - 3);
+        fr_t off_val = as[off_idx].val;
+        uint64_t off_var = as[off_idx].var;
+        fr_t c_val, t;
+        uint64_t c_var = num_public + nwit++;
+        if (i % 2 != 0) {
+            fr_add(&t, &b_val, &off_val);
+            fr_mul(&c_val, &a_val, &t);
+            cols[0] = a_var;
+            push_lc_row(&I->m[0], cols, 1, x);
+            cols[0] = b_var, cols[1] = off_var;
+            push_lc_row(&I->m[1], cols, 2, x);
+        } else {
+            fr_add(&t, &a_val, &b_val);
+            fr_add(&c_val, &t, &off_val);
+            cols[0] = a_var, cols[1] = b_var, cols[2] = off_var;
+            push_lc_row(&I->m[0], cols, 3, x);
+            cols[0] = 0;
+            push_lc_row(&I->m[1], cols, 1, x);
+        }
+        cols[0] = c_var;
+        push_lc_row(&I->m[2], cols, 1, x);
+        I->z[c_var] = c_val;
+        as[nas].var = c_var, as[nas].val = c_val, nas++;
+        a_val = b_val, a_var = b_var;
+        b_val = c_val, b_var = c_var;
+    }
+    uint64_t *lc = (uint64_t *)malloc(8 * (nas + 1));
+    for (uint64_t i = num_sparse; i < num_private; ++i, ++x) {
+        fr_t c_val;
+        fr_zero(&c_val);
+        for (size_t k = 0; k < nas; ++k) fr_add(&c_val, &c_val, &as[k].val);
+        fr_sqr(&c_val, &c_val);
+        uint64_t c_var = num_public + nwit++;
+        for (size_t k = 0; k < nas; ++k) lc[k] = as[k].var;
+        push_lc_row(&I->m[0], lc, nas, x);
+        for (size_t k = 0; k < nas; ++k) lc[k] = as[k].var;
+        push_lc_row(&I->m[1], lc, nas, x);
+        cols[0] = c_var;
+        push_lc_row(&I->m[2], cols, 1, x);
+        I->z[c_var] = c_val;
+    }
+    for (; x < n; ++x)
+        for (int k = 0; k < 3; ++k) I->m[k].row_ptr[x + 1] = I->m[k].nnz;
+    free(lc);
+    free(as);
+}
+
+static void gen_ragged(orc_inst *I, uint64_t seed, int max_row, int dense_rows) {
+    uint64_t n = I->n;
+    sm64 r = {seed};
+    fr_one(&I->z[0]);
+    for (uint64_t i = 1; i < n; ++i) sm64_fr(&r, &I->z[i]);
+    /* rows as lists first (dense rows replace whole rows afterwards) */
+    typedef struct { uint32_t *col; fr_t *val; uint64_t k; } row_t;
+    row_t *rows[3];
+    uint64_t *used = (uint64_t *)malloc(8 * (max_row + 1));
+    for (int m = 0; m < 3; ++m) {
+        rows[m] = (row_t *)calloc(n, sizeof(row_t));
+        for (uint64_t x = 0; x < n; ++x) {
+            uint64_t k = sm64_next(&r) % (uint64_t)(max_row + 1);
+            if (k > n) k = n;
+            uint64_t got = 0;
+            while (got < k) {
+                uint64_t y = sm64_next(&r) & (n - 1);
+                int dup = 0;
+                for (uint64_t q = 0; q < got; ++q) dup |= used[q] == y;
+                if (!dup) used[got++] = y;
+            }
+            rows[m][x].k = k;
+            rows[m][x].col = (uint32_t *)malloc(4 * (k ? k : 1));
+            rows[m][x].val = (fr_t *)malloc(sizeof(fr_t) * (k ? k : 1));
+            for (uint64_t q = 0; q < k; ++q) {
+                rows[m][x].col[q] = (uint32_t)used[q];
+                sm64_fr(&r, &rows[m][x].val[q]);
+            }
+        }
+    }
+    for (int d = 0; d < dense_rows; ++d) {
+        uint64_t x = sm64_next(&r) & (n - 1);
+        for (int m = 0; m < 2; ++m) {
+            row_t *rw = &rows[m][x];
+            free(rw->col);
+            free(rw->val);
+            rw->col = (uint32_t *)malloc(4 * n);
+            rw->val = (fr_t *)malloc(sizeof(fr_t) * n);
+            rw->k = 0;
+            for (uint64_t y = 0; y < n; ++y) {
+                if (sm64_next(&r) % 8 != 0) {
+                    rw->col[rw->k] = (uint32_t)y;
+                    sm64_fr(&r, &rw->val[rw->k]);
+                    rw->k++;
+                }
+            }
+        }
+    }
+    for (int m = 0; m < 3; ++m) {
+        mat_init(&I->m[m], n, n);
+        for (uint64_t x = 0; x < n; ++x) {
+            for (uint64_t q = 0; q < rows[m][x].k; ++q) mat_push(&I->m[m], rows[m][x].col[q], &rows[m][x].val[q]);
+            I->m[m].row_ptr[x + 1] = I->m[m].nnz;
+            free(rows[m][x].col);
+            free(rows[m][x].val);
+        }
+        free(rows[m]);
+    }
+    free(used);
+}
+
+orc_inst *orc_gen(int kind, int log_n, int log_v, uint64_t seed, uint64_t param) {
+    orc_inst *I = (orc_inst *)calloc(1, sizeof(orc_inst));
+    I->log_n = log_n;
+    I->log_v = log_v;
+    I->n = 1ULL << log_n;
+    I->z = (fr_t *)calloc(I->n, sizeof(fr_t));
+    if (kind == ORC_GEN_UNIFORM_3N)
+        gen_uniform_3n(I, seed);
+    else if (kind == ORC_GEN_REF_SHAPED)
+        gen_ref_shaped(I, seed, (int)param);
+    else
+        gen_ragged(I, seed, (int)(param & 0xFFFF), (int)(param >> 16));
+    return I;
+}
+uint64_t orc_inst_nnz(const orc_inst *I, int m) { return I->m[m].nnz; }
+int orc_inst_log_v(const orc_inst *I) { return I->log_v; }
+void orc_inst_export(const orc_inst *I, int m, uint64_t *row_ptr, uint32_t *col, uint8_t *val) {
+    const mat_t *M = &I->m[m];
+    if (row_ptr) memcpy(row_ptr, M->row_ptr, 8 * (I->n + 1));
+    if (col) memcpy(col, M->col, 4 * M->nnz);
+    if (val)
+        for (uint64_t i = 0; i < M->nnz; ++i) fr_to_bytes(val + 32 * i, &M->val[i]);
+}
+void orc_inst_z(const orc_inst *I, uint8_t *z) {
+    for (uint64_t i = 0; i < I->n; ++i) fr_to_bytes(z + 32 * i, &I->z[i]);
+}
+void orc_inst_free(orc_inst *I) {
+    if (!I) return;
+    for (int k = 0; k < 3; ++k) {
+        free(I->m[k].row_ptr);
+        free(I->m[k].col);
+        free(I->m[k].val);
+    }
+    free(I->z);
+    free(I);
+}
+
+/* ============================================================== byte buffers / serialization */
+typedef struct { uint8_t *p; size_t len, cap; } buf_t;
+static void buf_put(buf_t *b, const void *d, size_t k) {
+    if (b->len + k > b->cap) {
+        b->cap = (b->len + k) * 2 + 64;
+        b->p = (uint8_t *)realloc(b->p, b->cap);
+    }
+    memcpy(b->p + b->len, d, k);
+    b->len += k;
+}
+static void buf_u64(buf_t *b, uint64_t x) { buf_put(b, &x, 8); }
+static void buf_fr(buf_t *b, const fr_t *x) {
+    uint8_t t[32];
+    fr_to_bytes(t, x);
+    buf_put(b, t, 32);
+}
+static void fq_bytes(uint8_t *out48, const fq_t *x, uint8_t flags) {
+    uint64_t c[6];
+    fq_to_canon(c, x);
+    memcpy(out48, c, 48);
+    out48[47] |= flags;
+}
+#define FLAG_INF 0x40
+#define FLAG_POS 0x80
+static void g1_compress(uint8_t *out48, const g1_aff *a) {
+    if (a->inf) {
+        fq_t z;
+        fq_zero(&z);
+        fq_bytes(out48, &z, FLAG_INF);
+        return;
+    }
+    fq_t ny;
+    fq_neg(&ny, &a->y);
+    fq_bytes(out48, &a->x, fq_canon_gt(&a->y, &ny) ? FLAG_POS : 0);
+}
+static void g2_compress(uint8_t *out96, const g2_aff *a) {
+    if (a->inf) {
+        fq_t z;
+        fq_zero(&z);
+        fq_bytes(out96, &z, 0);
+        fq_bytes(out96 + 48, &z, FLAG_INF);
+        return;
+    }
+    fq2_t ny;
+    fq2_neg(&ny, &a->y);
+    fq_bytes(out96, &a->x.c0, 0);
+    fq_bytes(out96 + 48, &a->x.c1, fq2_canon_gt(&a->y, &ny) ? FLAG_POS : 0);
+}
+static int fq_from_bytes48(fq_t *r, const uint8_t *b, uint8_t *flags) {
+    uint64_t c[6];
+    memcpy(c, b, 48);
+    if (flags) *flags = (uint8_t)(c[5] >> 56) & 0xC0;
+    c[5] &= 0x3FFFFFFFFFFFFFFFULL;
+    if (fq_geq_p(c)) return -1;
+    fq_from_canon(r, c);
+    return 0;
+}
+static int g1_from_unc(g1_aff *a, const uint8_t *b) {
+    uint8_t f;
+    if (fq_from_bytes48(&a->x, b, NULL) || fq_from_bytes48(&a->y, b + 48, &f)) return -1;
+    a->inf = (f & FLAG_INF) != 0;
+    return 0;
+}
+static int g2_from_unc(g2_aff *a, const uint8_t *b) {
+    uint8_t f;
+    if (fq_from_bytes48(&a->x.c0, b, NULL) || fq_from_bytes48(&a->x.c1, b + 48, NULL) ||
+        fq_from_bytes48(&a->y.c0, b + 96, NULL) || fq_from_bytes48(&a->y.c1, b + 144, &f))
+        return -1;
+    a->inf = (f & FLAG_INF) != 0;
+    return 0;
+}
+static void g1_to_unc(uint8_t *b, const g1_aff *a) {
+    if (a->inf) {
+        fq_t z, o;
+        fq_zero(&z);
+        fq_one(&o);
+        fq_bytes(b, &z, 0);
+        fq_bytes(b + 48, &o, FLAG_INF);
+        return;
+    }
+    fq_bytes(b, &a->x, 0);
+    fq_bytes(b + 48, &a->y, 0);
+}
+static void g2_to_unc(uint8_t *b, const g2_aff *a) {
+    if (a->inf) {
+        fq_t z, o;
+        fq_zero(&z);
+        fq_one(&o);
+        fq_bytes(b, &z, 0);
+        fq_bytes(b + 48, &z, 0);
+        fq_bytes(b + 96, &o, 0);
+        fq_bytes(b + 144, &z, FLAG_INF);
+        return;
+    }
+    fq_bytes(b, &a->x.c0, 0);
+    fq_bytes(b + 48, &a->x.c1, 0);
+    fq_bytes(b + 96, &a->y.c0, 0);
+    fq_bytes(b + 144, &a->y.c1, 0);
+}
+
+/* ============================================================== transcript */
+typedef struct {
+    int injected;
+    ob2s_t st;
+    sm64 inj;
+} fs_t;
+static void fs_init(fs_t *f, int injected, uint64_t seed) {
+    f->injected = injected;
+    ob2s_init(&f->st);
+    f->inj.s = seed;
+}
+static void fs_feed(fs_t *f, const void *d, size_t k) {
+    if (!f->injected) ob2s_update(&f->st, d, k);
+}
+static void fs_fill(fs_t *f, uint8_t *dest, size_t n) {
+    uint8_t out[32];
+    ob2s_peek(&f->st, out);
+    size_t ptr = 0;
+    for (size_t i = 0; i < n; ++i) {
+        dest[i] = out[ptr++];
+        if (ptr == 32) {
+            ob2s_update(&f->st, out, 32);
+            ob2s_peek(&f->st, out);
+            ptr = 0;
+        }
+    }
+    ob2s_update(&f->st, out, 32);
+}
+/* Fr::rand: the accepted 4-limb bigint IS the Montgomery representation */
+static void fs_rand_fr(fs_t *f, fr_t *r) {
+    if (f->injected) {
+        sm64_fr(&f->inj, r);
+        return;
+    }
+    for (;;) {
+        uint64_t l[4];
+        for (int i = 0; i < 4; ++i) {
+            uint8_t b[8];
+            fs_fill(f, b, 8);
+            memcpy(&l[i], b, 8);
+        }
+        l[3] &= 0x7FFFFFFFFFFFFFFFULL;
+        if (!fr_geq_p(l)) {
+            memcpy(r->v, l, 32);
+            return;
+        }
+    }
+}
+
+/* ============================================================== VariableBaseMSM (ark-ec) */
+static int ark_log2(uint64_t x) { /* ceil(log2) */
+    if (x <= 1) return 0;
+    int l = 0;
+    uint64_t v = x - 1;
+    while (v) {
+        ++l;
+        v >>= 1;
+    }
+    return l;
+}
+static int msm_c(size_t n) { return n < 32 ? 3 : ark_log2(n) * 69 / 100 + 2; }
+static uint64_t digit(const uint64_t *s, int start, int c) {
+    int limb = start / 64, off = start % 64;
+    uint64_t d = s[limb] >> off;
+    if (off + c > 64 && limb + 1 < 4) d |= s[limb + 1] << (64 - off);
+    return d & ((1ULL << c) - 1);
+}
+static int canon_is_one(const uint64_t *s) { return s[0] == 1 && !s[1] && !s[2] && !s[3]; }
+static int canon_is_zero(const uint64_t *s) { return !(s[0] | s[1] | s[2] | s[3]); }
+
+#define DEFINE_MSM(G)                                                                         \
+    static void G##_msm(G##_jac *res_out, const G##_aff *bases, const uint64_t (*sc)[4], size_t n) { \
+        int c = msm_c(n);                                                                     \
+        int nb = 255;                                                                         \
+        int nw = (nb + c - 1) / c;                                                            \
+        G##_jac *ws = (G##_jac *)malloc(sizeof(G##_jac) * nw);                                \
+        G##_jac *bk = (G##_jac *)malloc(sizeof(G##_jac) * ((1u << c) - 1));                  \
+        for (int w = 0; w < nw; ++w) {                                                        \
+            int w_start = w * c;                                                              \
+            G##_jac res;                                                                      \
+            G##_set_inf(&res);                                                                \
+            for (size_t b = 0; b + 1 < (1u << c); ++b) G##_set_inf(&bk[b]);                   \
+            for (size_t i = 0; i < n; ++i) {                                                  \
+                if (canon_is_zero(sc[i])) continue;                                           \
+                if (canon_is_one(sc[i])) {                                                    \
+                    if (w_start == 0) G##_madd(&res, &res, &bases[i]);                        \
+                } else {                                                                      \
+                    uint64_t d = digit(sc[i], w_start, c);                                    \
+                    if (d) G##_madd(&bk[d - 1], &bk[d - 1], &bases[i]);                      \
+                }                                                                             \
+            }                                                                                 \
+            G##_jac run;                                                                      \
+            G##_set_inf(&run);                                                                \
+            for (size_t b = (1u << c) - 1; b-- > 0;) {                                        \
+                G##_add(&run, &run, &bk[b]);                                                  \
+                G##_add(&res, &res, &run);                                                    \
+            }                                                                                 \
+            ws[w] = res;                                                                      \
+        }                                                                                     \
+        G##_jac tot;                                                                          \
+        G##_set_inf(&tot);                                                                    \
+        for (int w = nw - 1; w >= 1; --w) {                                                   \
+            G##_add(&tot, &tot, &ws[w]);                                                      \
+            for (int k = 0; k < c; ++k) G##_dbl(&tot, &tot);                                  \
+        }                                                                                     \
+        G##_add(res_out, &tot, &ws[0]);                                                       \
+        free(ws);                                                                             \
+        free(bk);                                                                             \
+    }
+DEFINE_MSM(g1)
+DEFINE_MSM(g2)
+
+/* ============================================================== public parameters */
+struct orc_pp {
+    int nv;
+    g1_aff **pg; /* pg[i]: 2^(nv-i) points */
+    g2_aff **ph;
+    g1_aff g;
+    g2_aff h;
+    int has_t;
+    fr_t *t;
+};
+
+/* eq(t[0..k], x) table, x bit j <-> t[j] */
+static void eq_table(fr_t *out, const fr_t *t, int k) {
+    fr_one(&out[0]);
+    for (int j = 0; j < k; ++j) {
+        size_t half = (size_t)1 << j;
+        fr_t one, om;
+        fr_one(&one);
+        fr_sub(&om, &one, &t[j]);
+        for (size_t x = half; x-- > 0;) {
+            fr_mul(&out[x + half], &out[x], &t[j]);
+            fr_mul(&out[x], &out[x], &om);
+        }
+    }
+}
+
+#define DEFINE_FIXED_BASE(G)                                                                  \
+    /* ark-ec FixedBaseMSM semantics: out[i] = s_i * base (affine) */                         \
+    static void G##_fixed_base(G##_aff *out, const G##_aff *base, const fr_t *s, size_t n) {  \
+        const int c = 8, nw = 32;                                                             \
+        G##_aff *tab = (G##_aff *)malloc(sizeof(G##_aff) * nw * 256);                         \
+        G##_jac *tj = (G##_jac *)malloc(sizeof(G##_jac) * 256);                               \
+        G##_jac outer;                                                                        \
+        G##_from_aff(&outer, base);                                                           \
+        for (int w = 0; w < nw; ++w) {                                                        \
+            G##_set_inf(&tj[0]);                                                              \
+            for (int d = 1; d < 256; ++d) G##_add(&tj[d], &tj[d - 1], &outer);               \
+            G##_batch_to_aff(tab + 256 * w, tj, 256);                                         \
+            for (int k = 0; k < c; ++k) G##_dbl(&outer, &outer);                              \
+        }                                                                                     \
+        G##_jac *res = (G##_jac *)malloc(sizeof(G##_jac) * (n ? n : 1));                      \
+        for (size_t i = 0; i < n; ++i) {                                                      \
+            uint64_t cs[4];                                                                   \
+            fr_to_canon(cs, &s[i]);                                                           \
+            G##_set_inf(&res[i]);                                                             \
+            for (int w = 0; w < nw; ++w) {                                                    \
+                uint64_t d = digit(cs, w * c, c);                                             \
+                if (d) G##_madd(&res[i], &res[i], &tab[256 * w + d]);                         \
+            }                                                                                 \
+        }                                                                                     \
+        G##_batch_to_aff(out, res, n);                                                        \
+        free(res);                                                                            \
+        free(tj);                                                                             \
+        free(tab);                                                                            \
+    }
+DEFINE_FIXED_BASE(g1)
+DEFINE_FIXED_BASE(g2)
+
+static void pp_alloc(orc_pp *pp, int nv) {
+    pp->nv = nv;
+    pp->pg = (g1_aff **)calloc(nv ? nv : 1, sizeof(void *));
+    pp->ph = (g2_aff **)calloc(nv ? nv : 1, sizeof(void *));
+    for (int i = 0; i < nv; ++i) {
+        pp->pg[i] = (g1_aff *)malloc(sizeof(g1_aff) << (nv - i));
+        pp->ph[i] = (g2_aff *)malloc(sizeof(g2_aff) << (nv - i));
+    }
+}
+
+orc_pp *orc_keygen(int nv, uint64_t seed) {
+    sm64 r = {seed};
+    fr_t gs, hs;
+    sm64_fr(&r, &gs);
+    sm64_fr(&r, &hs);
+    orc_pp *pp = (orc_pp *)calloc(1, sizeof(orc_pp));
+    pp_alloc(pp, nv);
+    pp->t = (fr_t *)malloc(sizeof(fr_t) * (nv ? nv : 1));
+    for (int i = 0; i < nv; ++i) sm64_fr(&r, &pp->t[i]);
+    pp->has_t = 1;
+    g1_aff gg = {.inf = 0};
+    g2_aff hg = {.inf = 0};
+    static const uint64_t G1X[6] = {0x5cb38790fd530c16ULL, 0x7817fc679976fff5ULL, 0x154f95c7143ba1c1ULL, 0xf0ae6acdf3d0e747ULL, 0xedce6ecc21dbf440ULL, 0x120177419e0bfb75ULL};
+    static const uint64_t G1Y[6] = {0xbaac93d50ce72271ULL, 0x8c22631a7918fd8eULL, 0xdd595f13570725ceULL, 0x51ac582950405194ULL, 0x0e1c8c3fad0059c0ULL, 0x0bbc3efc5008a26aULL};
+    static const uint64_t G2X0[6] = {0xf5f28fa202940a10ULL, 0xb3f5fb2687b4961aULL, 0xa1a893b53e2ae580ULL, 0x9894999d1a3caee9ULL, 0x6f67b7631863366bULL, 0x058191924350bcd7ULL};
+    static const uint64_t G2X1[6] = {0xa5a9c0759e23f606ULL, 0xaaa0c59dbccd60c3ULL, 0x3bb17e18e2867806ULL, 0x1b1ab6cc8541b367ULL, 0xc2b6ed0ef2158547ULL, 0x11922a097360edf3ULL};
+    static const uint64_t G2Y0[6] = {0x4c730af860494c4aULL, 0x597cfa1f5e369c5aULL, 0xe7e6856caa0a635aULL, 0xbbefb5e96e0d495fULL, 0x07d3a975f0ef25a2ULL, 0x0083fd8e7e80dae5ULL};
+    static const uint64_t G2Y1[6] = {0xadc0fc92df64b05dULL, 0x18aa270a2b1461dcULL, 0x86adac6a3be4eba0ULL, 0x79495c4ec93da33aULL, 0xe7175850a43ccaedULL, 0x0b2bc2a163de1bf2ULL};
+    memcpy(gg.x.v, G1X, 48);
+    memcpy(gg.y.v, G1Y, 48);
+    memcpy(hg.x.c0.v, G2X0, 48);
+    memcpy(hg.x.c1.v, G2X1, 48);
+    memcpy(hg.y.c0.v, G2Y0, 48);
+    memcpy(hg.y.c1.v, G2Y1, 48);
+    g1_jac gj;
+    g2_jac hj;
+    uint64_t c[4];
+    g1_from_aff(&gj, &gg);
+    fr_to_canon(c, &gs);
+    g1_mul_canon(&gj, &gj, c);
+    g1_to_aff(&pp->g, &gj);
+    g2_from_aff(&hj, &hg);
+    fr_to_canon(c, &hs);
+    g2_mul_canon(&hj, &hj, c);
+    g2_to_aff(&pp->h, &hj);
+    /* pp_powers: concatenation over levels of eq(t[i..], x) (setup.rs:37-60) */
+    size_t total = 0;
+    for (int i = 0; i < nv; ++i) total += (size_t)1 << (nv - i);
+    fr_t *pw = (fr_t *)malloc(sizeof(fr_t) * (total ? total : 1));
+    size_t off = 0;
+    for (int i = 0; i < nv; ++i) {
+        eq_table(pw + off, pp->t + i, nv - i);
+        off += (size_t)1 << (nv - i);
+    }
+    g1_aff *ag = (g1_aff *)malloc(sizeof(g1_aff) * (total ? total : 1));
+    g2_aff *ah = (g2_aff *)malloc(sizeof(g2_aff) * (total ? total : 1));
+    g1_fixed_base(ag, &pp->g, pw, total);
+    g2_fixed_base(ah, &pp->h, pw, total);
+    off = 0;
+    for (int i = 0; i < nv; ++i) {
+        size_t k = (size_t)1 << (nv - i);
+        memcpy(pp->pg[i], ag + off, sizeof(g1_aff) * k);
+        memcpy(pp->ph[i], ah + off, sizeof(g2_aff) * k);
+        off += k;
+    }
+    free(ag);
+    free(ah);
+    free(pw);
+    return pp;
+}
+
+size_t orc_pp_serialize(const orc_pp *pp, uint8_t *out, size_t cap) {
+    int nv = pp->nv;
+    size_t need = 8 + 8 + 8 + 96 + 192;
+    for (int i = 0; i < nv; ++i) need += 16 + (96 + 192) * ((size_t)1 << (nv - i));
+    if (!out || cap < need) return need;
+    uint8_t *p = out;
+    uint64_t u = (uint64_t)nv;
+    memcpy(p, &u, 8), p += 8;
+    memcpy(p, &u, 8), p += 8;
+    for (int i = 0; i < nv; ++i) {
+        uint64_t k = 1ULL << (nv - i);
+        memcpy(p, &k, 8), p += 8;
+        for (uint64_t j = 0; j < k; ++j) g1_to_unc(p, &pp->pg[i][j]), p += 96;
+    }
+    memcpy(p, &u, 8), p += 8;
+    for (int i = 0; i < nv; ++i) {
+        uint64_t k = 1ULL << (nv - i);
+        memcpy(p, &k, 8), p += 8;
+        for (uint64_t j = 0; j < k; ++j) g2_to_unc(p, &pp->ph[i][j]), p += 192;
+    }
+    g1_to_unc(p, &pp->g), p += 96;
+    g2_to_unc(p, &pp->h), p += 192;
+    return need;
+}
+
+orc_pp *orc_pp_load(const uint8_t *b, size_t len) {
+    size_t pos = 0;
+#define NEED(k)                                     \
+    do {                                            \
+        if (pos + (k) > len) goto fail;             \
+    } while (0)
+    orc_pp *pp = (orc_pp *)calloc(1, sizeof(orc_pp));
+    uint64_t nv, cnt;
+    NEED(16);
+    memcpy(&nv, b, 8);
+    memcpy(&cnt, b + 8, 8);
+    pos = 16;
+    if (nv > 40 || cnt != nv) goto fail;
+    pp_alloc(pp, (int)nv);
+    for (uint64_t i = 0; i < nv; ++i) {
+        uint64_t k;
+        NEED(8);
+        memcpy(&k, b + pos, 8), pos += 8;
+        if (k != (1ULL << (nv - i))) goto fail;
+        NEED(96 * k);
+        for (uint64_t j = 0; j < k; ++j)
+            if (g1_from_unc(&pp->pg[i][j], b + pos + 96 * j)) goto fail;
+        pos += 96 * k;
+    }
+    NEED(8);
+    memcpy(&cnt, b + pos, 8), pos += 8;
+    if (cnt != nv) goto fail;
+    for (uint64_t i = 0; i < nv; ++i) {
+        uint64_t k;
+        NEED(8);
+        memcpy(&k, b + pos, 8), pos += 8;
+        if (k != (1ULL << (nv - i))) goto fail;
+        NEED(192 * k);
+        for (uint64_t j = 0; j < k; ++j)
+            if (g2_from_unc(&pp->ph[i][j], b + pos + 192 * j)) goto fail;
+        pos += 192 * k;
+    }
+    NEED(96 + 192);
+    if (g1_from_unc(&pp->g, b + pos) || g2_from_unc(&pp->h, b + pos + 96)) goto fail;
+    return pp;
+fail:
+    set_err("malformed public parameter bytes");
+    orc_pp_free(pp);
+    return NULL;
+#undef NEED
+}
+
+void orc_pp_trapdoor(const orc_pp *pp, uint8_t *t_out) {
+    for (int i = 0; i < pp->nv; ++i) {
+        if (pp->has_t)
+            fr_to_bytes(t_out + 32 * i, &pp->t[i]);
+        else
+            memset(t_out + 32 * i, 0, 32);
+    }
+}
+
+void orc_pp_free(orc_pp *pp) {
+    if (!pp) return;
+    for (int i = 0; i < pp->nv; ++i) {
+        if (pp->pg) free(pp->pg[i]);
+        if (pp->ph) free(pp->ph[i]);
+    }
+    free(pp->pg);
+    free(pp->ph);
+    free(pp->t);
+    free(pp);
+}
+
+/* ============================================================== MLE / R1CS helpers */
+static void fix_first(fr_t *t, size_t len, const fr_t *r) { /* in place: t[b] <- t[2b](1-r)+t[2b+1]r */
+    fr_t one, om, a, b;
+    fr_one(&one);
+    fr_sub(&om, &one, r);
+    for (size_t i = 0; i < len / 2; ++i) {
+        fr_mul(&a, &t[2 * i], &om);
+        fr_mul(&b, &t[2 * i + 1], r);
+        fr_add(&t[i], &a, &b);
+    }
+}
+static void mle_eval(fr_t *out, const fr_t *table, int nv, const fr_t *pt) {
+    size_t n = (size_t)1 << nv;
+    fr_t *t = (fr_t *)malloc(sizeof(fr_t) * n);
+    memcpy(t, table, sizeof(fr_t) * n);
+    for (int i = 0; i < nv; ++i) fix_first(t, n >> i, &pt[i]);
+    *out = t[0];
+    free(t);
+}
+
+typedef struct {
+    uint64_t n;
+    const uint64_t *rp;
+    const uint32_t *col;
+    fr_t *val;
+} mtx_t;
+static int mtx_from_csr(mtx_t *m, const orc_csr *c) {
+    m->n = c->n;
+    m->rp = c->row_ptr;
+    m->col = c->col;
+    uint64_t nnz = c->row_ptr[c->n];
+    m->val = (fr_t *)malloc(sizeof(fr_t) * (nnz ? nnz : 1));
+    for (uint64_t i = 0; i < nnz; ++i)
+        if (fr_from_bytes(&m->val[i], c->val + 32 * i)) return -1;
+    return 0;
+}
+
+static void sum_over_y(fr_t *out, const mtx_t *M, const fr_t *z) {
+    for (uint64_t x = 0; x < M->n; ++x) {
+        fr_t acc, t;
+        fr_zero(&acc);
+        for (uint64_t k = M->rp[x]; k < M->rp[x + 1]; ++k) {
+            fr_mul(&t, &M->val[k], &z[M->col[k]]);
+            fr_add(&acc, &acc, &t);
+        }
+        out[x] = acc;
+    }
+}
+
+/* open-addressing map u64 -> fr (SparseMLExtensionMap's hash map) */
+typedef struct { uint64_t *key; fr_t *val; uint8_t *used; size_t cap, cnt; } hmap;
+static void hm_init(hmap *h, size_t want) {
+    size_t cap = 16;
+    while (cap < 2 * want + 2) cap <<= 1;
+    h->cap = cap;
+    h->cnt = 0;
+    h->key = (uint64_t *)malloc(8 * cap);
+    h->val = (fr_t *)malloc(sizeof(fr_t) * cap);
+    h->used = (uint8_t *)calloc(cap, 1);
+}
+static void hm_free(hmap *h) {
+    free(h->key);
+    free(h->val);
+    free(h->used);
+}
+static size_t hm_slot(const hmap *h, uint64_t k) {
+    uint64_t x = k * 0x9E3779B97F4A7C15ULL;
+    size_t i = (size_t)(x >> 17) & (h->cap - 1);
+    while (h->used[i] && h->key[i] != k) i = (i + 1) & (h->cap - 1);
+    return i;
+}
+static void hm_insert(hmap *h, uint64_t k, const fr_t *v) { /* overwrite */
+    size_t i = hm_slot(h, k);
+    if (!h->used[i]) h->used[i] = 1, h->key[i] = k, h->cnt++;
+    h->val[i] = *v;
+}
+static void hm_addto(hmap *h, uint64_t k, const fr_t *v) {
+    size_t i = hm_slot(h, k);
+    if (!h->used[i]) {
+        h->used[i] = 1, h->key[i] = k, h->cnt++;
+        h->val[i] = *v;
+    } else
+        fr_add(&h->val[i], &h->val[i], v);
+}
+
+static void eval_on_x(fr_t *out, const mtx_t *M, const fr_t *r_x, int s) {
+    uint64_t nnz = M->rp[M->n];
+    hmap cur;
+    hm_init(&cur, nnz);
+    for (uint64_t x = 0; x < M->n; ++x)
+        for (uint64_t k = M->rp[x]; k < M->rp[x + 1]; ++k) hm_insert(&cur, ((uint64_t)M->col[k] << s) + x, &M->val[k]);
+    for (int i = 0; i < s; ++i) {
+        hmap nxt;
+        hm_init(&nxt, cur.cnt);
+        fr_t one, om, w;
+        fr_one(&one);
+        fr_sub(&om, &one, &r_x[i]);
+        for (size_t j = 0; j < cur.cap; ++j) {
+            if (!cur.used[j]) continue;
+            fr_mul(&w, &cur.val[j], (cur.key[j] & 1) ? &r_x[i] : &om);
+            hm_addto(&nxt, cur.key[j] >> 1, &w);
+        }
+        hm_free(&cur);
+        cur = nxt;
+    }
+    for (uint64_t y = 0; y < M->n; ++y) fr_zero(&out[y]);
+    for (size_t j = 0; j < cur.cap; ++j)
+        if (cur.used[j]) out[cur.key[j]] = cur.val[j];
+    hm_free(&cur);
+}
+
+/* ============================================================== faithful sumcheck */
+typedef struct {
+    int ntab;       /* distinct tables (each folded once per round) */
+    fr_t **tab;
+    int nprod;
+    int plen[4];
+    int pidx[4][64]; /* product -> table indices */
+    int nv, max_mult, round;
+    size_t len;      /* current table length */
+    fr_t *rand;
+} mlsc_t;
+
+static void sc_info(buf_t *b, const mlsc_t *s) {
+    buf_u64(b, (uint64_t)s->max_mult); /* IndexInfo.max_multiplicands (reconstructed order) */
+    buf_u64(b, (uint64_t)s->nv);       /* IndexInfo.num_variables */
+}
+/* AHPForMLSumcheck::prove_round [upstream]; evals has max_mult + 1 entries */
+static void sc_round(mlsc_t *s, const fr_t *challenge, fr_t *evals) {
+    if (challenge) {
+        s->rand[s->round - 1] = *challenge;
+        for (int k = 0; k < s->ntab; ++k) fix_first(s->tab[k], s->len, challenge);
+        s->len /= 2;
+    }
+    s->round++;
+    int deg = s->max_mult;
+    fr_t one, tf[70], omt[70];
+    fr_one(&one);
+    fr_zero(&tf[0]);
+    for (int t = 0; t <= deg; ++t) {
+        if (t) fr_add(&tf[t], &tf[t - 1], &one);
+        fr_sub(&omt[t], &one, &tf[t]);
+        fr_zero(&evals[t]);
+    }
+    size_t half = s->len / 2;
+    for (size_t b = 0; b < half; ++b) {
+        for (int t = 0; t <= deg; ++t) {
+            for (int p = 0; p < s->nprod; ++p) {
+                fr_t prod, u, v;
+                fr_one(&prod);
+                for (int j = 0; j < s->plen[p]; ++j) {
+                    const fr_t *tb = s->tab[s->pidx[p][j]];
+                    fr_mul(&u, &tb[2 * b], &omt[t]);
+                    fr_mul(&v, &tb[2 * b + 1], &tf[t]);
+                    fr_add(&u, &u, &v);
+                    fr_mul(&prod, &prod, &u);
+                }
+                fr_add(&evals[t], &evals[t], &prod);
+            }
+        }
+    }
+}
+
+/* ============================================================== mKZG */
+static void to_canon_arr(uint64_t (*out)[4], const fr_t *a, size_t n) {
+    for (size_t i = 0; i < n; ++i) fr_to_canon(out[i], &a[i]);
+}
+static void commit(buf_t *b, const orc_pp *pp, const fr_t *z, int nv) {
+    size_t n = (size_t)1 << nv;
+    uint64_t(*sc)[4] = malloc(32 * n);
+    to_canon_arr(sc, z, n);
+    g1_jac r;
+    g1_msm(&r, pp->pg[0], (const uint64_t(*)[4])sc, n);
+    g1_aff a;
+    g1_to_aff(&a, &r);
+    buf_u64(b, (uint64_t)nv);
+    uint8_t c[48];
+    g1_compress(c, &a);
+    buf_put(b, c, 48);
+    free(sc);
+}
+/* open.rs:19-58; writes eval (Fr) then Proof{h, proofs} */
+static void open_(buf_t *b, fr_t *eval_out, const orc_pp *pp, const fr_t *z, int nv, const fr_t *pt) {
+    size_t n = (size_t)1 << nv;
+    mle_eval(eval_out, z, nv, pt);
+    fr_t *r = (fr_t *)malloc(sizeof(fr_t) * n);
+    memcpy(r, z, sizeof(fr_t) * n);
+    fr_t *q = (fr_t *)malloc(sizeof(fr_t) * (n / 2 + 1));
+    uint64_t(*sc)[4] = malloc(32 * n);
+    uint8_t *proofs = (uint8_t *)malloc(96 * (nv + 1));
+    for (int i = 0; i < nv; ++i) {
+        int k = nv - i;
+        size_t h = (size_t)1 << (k - 1);
+        fr_t one, om, a, c;
+        fr_one(&one);
+        fr_sub(&om, &one, &pt[i]);
+        for (size_t bb = 0; bb < h; ++bb) {
+            fr_sub(&q[bb], &r[2 * bb + 1], &r[2 * bb]);
+            fr_mul(&a, &r[2 * bb], &om);
+            fr_mul(&c, &r[2 * bb + 1], &pt[i]);
+            fr_add(&r[bb], &a, &c);
+        }
+        for (size_t x = 0; x < ((size_t)1 << k); ++x) fr_to_canon(sc[x], &q[x >> 1]);
+        g2_jac pj;
+        g2_msm(&pj, pp->ph[i], (const uint64_t(*)[4])sc, (size_t)1 << k);
+        g2_aff pa;
+        g2_to_aff(&pa, &pj);
+        g2_compress(proofs + 96 * i, &pa);
+    }
+    uint8_t hb[96];
+    g2_compress(hb, &pp->h);
+    buf_put(b, hb, 96);
+    buf_u64(b, (uint64_t)nv);
+    buf_put(b, proofs, 96 * (size_t)nv);
+    free(proofs);
+    free(sc);
+    free(q);
+    free(r);
+}
+
+/* ============================================================== exported kernel-level checkers */
+static fr_t *frs_from_bytes(const uint8_t *b, size_t n) {
+    fr_t *a = (fr_t *)malloc(sizeof(fr_t) * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) fr_from_bytes(&a[i], b + 32 * i);
+    return a;
+}
+void orc_sum_over_y(const orc_csr *M, const uint8_t *z, uint8_t *out) {
+    mtx_t m;
+    mtx_from_csr(&m, M);
+    fr_t *zz = frs_from_bytes(z, M->n), *o = (fr_t *)malloc(sizeof(fr_t) * M->n);
+    sum_over_y(o, &m, zz);
+    for (uint64_t i = 0; i < M->n; ++i) fr_to_bytes(out + 32 * i, &o[i]);
+    free(o), free(zz), free(m.val);
+}
+void orc_eval_on_x(const orc_csr *M, const uint8_t *r_x, uint8_t *out) {
+    mtx_t m;
+    mtx_from_csr(&m, M);
+    int s = ark_log2(M->n);
+    fr_t *r = frs_from_bytes(r_x, (size_t)s), *o = (fr_t *)malloc(sizeof(fr_t) * M->n);
+    eval_on_x(o, &m, r, s);
+    for (uint64_t i = 0; i < M->n; ++i) fr_to_bytes(out + 32 * i, &o[i]);
+    free(o), free(r), free(m.val);
+}
+void orc_msm_g1(const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out) {
+    g1_aff *b = (g1_aff *)malloc(sizeof(g1_aff) * (n ? n : 1));
+    uint64_t(*sc)[4] = malloc(32 * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) {
+        g1_from_unc(&b[i], bases + 96 * i);
+        memcpy(sc[i], scalars + 32 * i, 32);
+    }
+    g1_jac r;
+    g1_msm(&r, b, (const uint64_t(*)[4])sc, n);
+    g1_aff a;
+    g1_to_aff(&a, &r);
+    g1_to_unc(out, &a);
+    free(sc), free(b);
+}
+void orc_msm_g2(const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out) {
+    g2_aff *b = (g2_aff *)malloc(sizeof(g2_aff) * (n ? n : 1));
+    uint64_t(*sc)[4] = malloc(32 * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) {
+        g2_from_unc(&b[i], bases + 192 * i);
+        memcpy(sc[i], scalars + 32 * i, 32);
+    }
+    g2_jac r;
+    g2_msm(&r, b, (const uint64_t(*)[4])sc, n);
+    g2_aff a;
+    g2_to_aff(&a, &r);
+    g2_to_unc(out, &a);
+    free(sc), free(b);
+}
+void orc_commit(const orc_pp *pp, const uint8_t *table, int nv, uint8_t *out56) {
+    fr_t *z = frs_from_bytes(table, (size_t)1 << nv);
+    buf_t b = {0};
+    commit(&b, pp, z, nv);
+    memcpy(out56, b.p, 56);
+    free(b.p), free(z);
+}
+void orc_open(const orc_pp *pp, const uint8_t *table, int nv, const uint8_t *point, uint8_t *eval_out,
+              uint8_t *proof_out) {
+    fr_t *z = frs_from_bytes(table, (size_t)1 << nv), *pt = frs_from_bytes(point, (size_t)nv), ev;
+    buf_t b = {0};
+    open_(&b, &ev, pp, z, nv, pt);
+    fr_to_bytes(eval_out, &ev);
+    memcpy(proof_out, b.p, b.len);
+    free(b.p), free(z), free(pt);
+}
+
+/* ============================================================== the argument */
+static void feed_matrix(fs_t *f, const orc_csr *M) {
+    /* MatrixExtension: Vec<Vec<(Fr, usize)>> then num_constraints: usize — streamed */
+    uint8_t rec[40];
+    uint64_t n = M->n, k;
+    fs_feed(f, &n, 8);
+    for (uint64_t x = 0; x < n; ++x) {
+        k = M->row_ptr[x + 1] - M->row_ptr[x];
+        fs_feed(f, &k, 8);
+        for (uint64_t j = M->row_ptr[x]; j < M->row_ptr[x + 1]; ++j) {
+            uint64_t col = M->col[j];
+            memcpy(rec, M->val + 32 * j, 32);
+            memcpy(rec + 32, &col, 8);
+            fs_feed(f, rec, 40);
+        }
+    }
+    fs_feed(f, &n, 8);
+}
+
+int orc_prove(const orc_csr *A, const orc_csr *B, const orc_csr *C, const uint8_t *v, size_t nv_len,
+              const uint8_t *w, size_t nw_len, const orc_pp *pp, int mode, uint64_t inj_seed, uint8_t *out,
+              size_t cap, size_t *out_len) {
+    uint64_t n = A->n;
+    if (!n || (n & (n - 1))) return set_err("Matrix width should be a power of 2."), 1;
+    if (B->n != n || C->n != n) return set_err("matrix size is inconsistent with number of constraints"), 1;
+    const orc_csr *Ms[3] = {A, B, C};
+    for (int m = 0; m < 3; ++m)
+        for (uint64_t k = 0; k < Ms[m]->row_ptr[n]; ++k)
+            if (Ms[m]->col[k] >= n) return set_err("sparse index out of bound"), 1;
+    int log_n = ark_log2(n);
+    if (!nv_len || (nv_len & (nv_len - 1))) return set_err("public input should be power of two"), 1;
+    if (nv_len + nw_len != n) return set_err("|v| + |w| != number of variables"), 1;
+    if (pp->nv < log_n) return set_err("public parameter too small"), 1;
+    int log_v = ark_log2(nv_len);
+    fs_t fs;
+    fs_init(&fs, mode == 1, inj_seed);
+    for (int m = 0; m < 3; ++m) feed_matrix(&fs, Ms[m]);
+    uint64_t u = nv_len;
+    fs_feed(&fs, &u, 8);
+    fs_feed(&fs, v, 32 * nv_len);
+    mtx_t mt[3];
+    for (int m = 0; m < 3; ++m)
+        if (mtx_from_csr(&mt[m], Ms[m])) return set_err("non-canonical field element"), 1;
+    fr_t *z = (fr_t *)malloc(sizeof(fr_t) * n);
+    for (size_t i = 0; i < nv_len; ++i)
+        if (fr_from_bytes(&z[i], v + 32 * i)) return set_err("non-canonical field element"), 1;
+    for (size_t i = 0; i < nw_len; ++i)
+        if (fr_from_bytes(&z[nv_len + i], w + 32 * i)) return set_err("non-canonical field element"), 1;
+    /* the PP used is the level-aligned suffix when pp->nv > log_n is not supported by the
+       reference either (open indexes powers_of_h[i] with 2^(nv-i) points): require equality */
+    if (pp->nv != log_n) return set_err("public parameter nv != log_n"), 1;
+    buf_t pf = {0};
+    size_t mark;
+    /* round 1: commit */
+    mark = pf.len;
+    commit(&pf, pp, z, log_n);
+    fs_feed(&fs, pf.p + mark, pf.len - mark);
+    fr_t *pt = (fr_t *)calloc(log_n, sizeof(fr_t));
+    for (int i = 0; i < log_v; ++i) fs_rand_fr(&fs, &pt[i]);
+    /* round 2: open at (r_v, 0...) */
+    mark = pf.len;
+    fr_t ev;
+    buf_t ob = {0};
+    open_(&ob, &ev, pp, z, log_n, pt);
+    buf_fr(&pf, &ev);
+    buf_put(&pf, ob.p, ob.len);
+    free(ob.p);
+    fs_feed(&fs, pf.p + mark, pf.len - mark);
+    fr_t *tau = (fr_t *)malloc(sizeof(fr_t) * log_n);
+    for (int i = 0; i < log_n; ++i) fs_rand_fr(&fs, &tau[i]);
+    /* round 3: eq tables (log_n of them), SpMVs, sumcheck #1 setup */
+    mlsc_t sc;
+    memset(&sc, 0, sizeof sc);
+    sc.ntab = 3 + log_n;
+    sc.tab = (fr_t **)malloc(sizeof(fr_t *) * sc.ntab);
+    for (int k = 0; k < sc.ntab; ++k) sc.tab[k] = (fr_t *)malloc(sizeof(fr_t) * n);
+    fr_t *az = (fr_t *)malloc(sizeof(fr_t) * n), *bz = (fr_t *)malloc(sizeof(fr_t) * n),
+         *cz = (fr_t *)malloc(sizeof(fr_t) * n);
+    sum_over_y(az, &mt[0], z);
+    sum_over_y(bz, &mt[1], z);
+    sum_over_y(cz, &mt[2], z);
+    memcpy(sc.tab[0], az, sizeof(fr_t) * n);
+    memcpy(sc.tab[1], bz, sizeof(fr_t) * n);
+    for (uint64_t x = 0; x < n; ++x) fr_neg(&sc.tab[2][x], &cz[x]);
+    for (int i = 0; i < log_n; ++i) { /* eq.rs:8-17 */
+        fr_t one, t2, a;
+        fr_one(&one);
+        for (uint64_t x = 0; x < n; ++x) {
+            if ((x >> i) & 1) { /* 2 t - 1 - t + 1 = t */
+                fr_add(&t2, &tau[i], &tau[i]);
+                fr_sub(&a, &t2, &one);
+                fr_sub(&a, &a, &tau[i]);
+                fr_add(&sc.tab[3 + i][x], &a, &one);
+            } else { /* 0 - 0 - t + 1 */
+                fr_sub(&sc.tab[3 + i][x], &one, &tau[i]);
+            }
+        }
+    }
+    sc.nprod = 2;
+    sc.plen[0] = 2 + log_n;
+    sc.pidx[0][0] = 0, sc.pidx[0][1] = 1;
+    sc.plen[1] = 1 + log_n;
+    sc.pidx[1][0] = 2;
+    for (int i = 0; i < log_n; ++i) sc.pidx[0][2 + i] = 3 + i, sc.pidx[1][1 + i] = 3 + i;
+    sc.nv = log_n;
+    sc.max_mult = 2 + log_n;
+    sc.len = n;
+    sc.rand = (fr_t *)malloc(sizeof(fr_t) * (log_n + 1));
+    mark = pf.len;
+    sc_info(&pf, &sc);
+    fs_feed(&fs, pf.p + mark, pf.len - mark);
+    /* sumcheck #1 (lib.rs:86-103) */
+    buf_u64(&pf, (uint64_t)log_n);
+    fr_t ch, *evals = (fr_t *)malloc(sizeof(fr_t) * (sc.max_mult + 1));
+    fr_t *r_x = (fr_t *)malloc(sizeof(fr_t) * log_n);
+    for (int rnd = 0; rnd < log_n; ++rnd) {
+        sc_round(&sc, rnd ? &ch : NULL, evals);
+        mark = pf.len;
+        buf_u64(&pf, (uint64_t)(sc.max_mult + 1));
+        for (int t = 0; t <= sc.max_mult; ++t) buf_fr(&pf, &evals[t]);
+        fs_feed(&fs, pf.p + mark, pf.len - mark);
+        fs_rand_fr(&fs, &ch);
+        r_x[rnd] = ch;
+    }
+    for (int k = 0; k < sc.ntab; ++k) free(sc.tab[k]);
+    free(sc.tab);
+    /* round 4: va, vb, vc */
+    fr_t va, vb, vc;
+    mle_eval(&va, az, log_n, r_x);
+    mle_eval(&vb, bz, log_n, r_x);
+    mle_eval(&vc, cz, log_n, r_x);
+    mark = pf.len;
+    buf_fr(&pf, &va), buf_fr(&pf, &vb), buf_fr(&pf, &vc);
+    fs_feed(&fs, pf.p + mark, pf.len - mark);
+    fr_t rabc[3];
+    for (int i = 0; i < 3; ++i) fs_rand_fr(&fs, &rabc[i]);
+    /* round 5: eval_on_x, scaled; sumcheck #2 over 3 products of 2 */
+    mlsc_t s2;
+    memset(&s2, 0, sizeof s2);
+    s2.ntab = 4;
+    s2.tab = (fr_t **)malloc(sizeof(fr_t *) * 4);
+    for (int m = 0; m < 3; ++m) {
+        s2.tab[m] = (fr_t *)malloc(sizeof(fr_t) * n);
+        eval_on_x(s2.tab[m], &mt[m], r_x, log_n);
+        for (uint64_t y = 0; y < n; ++y) fr_mul(&s2.tab[m][y], &s2.tab[m][y], &rabc[m]);
+    }
+    s2.tab[3] = (fr_t *)malloc(sizeof(fr_t) * n);
+    memcpy(s2.tab[3], z, sizeof(fr_t) * n);
+    s2.nprod = 3;
+    for (int p = 0; p < 3; ++p) s2.plen[p] = 2, s2.pidx[p][0] = p, s2.pidx[p][1] = 3;
+    s2.nv = log_n;
+    s2.max_mult = 2;
+    s2.len = n;
+    s2.rand = (fr_t *)malloc(sizeof(fr_t) * (log_n + 1));
+    mark = pf.len;
+    sc_info(&pf, &s2);
+    fs_feed(&fs, pf.p + mark, pf.len - mark);
+    buf_u64(&pf, (uint64_t)log_n);
+    fr_t *r_y = (fr_t *)malloc(sizeof(fr_t) * log_n);
+    for (int rnd = 0; rnd < log_n; ++rnd) {
+        sc_round(&s2, rnd ? &ch : NULL, evals);
+        mark = pf.len;
+        buf_u64(&pf, 3);
+        for (int t = 0; t < 3; ++t) buf_fr(&pf, &evals[t]);
+        fs_feed(&fs, pf.p + mark, pf.len - mark);
+        fs_rand_fr(&fs, &ch);
+        r_y[rnd] = ch;
+    }
+    for (int k = 0; k < 4; ++k) free(s2.tab[k]);
+    free(s2.tab);
+    /* round 6: open at r_y */
+    buf_t ob2 = {0};
+    open_(&ob2, &ev, pp, z, log_n, r_y);
+    buf_fr(&pf, &ev);
+    buf_put(&pf, ob2.p, ob2.len);
+    free(ob2.p);
+    *out_len = pf.len;
+    int rc = 0;
+    if (out && cap >= pf.len)
+        memcpy(out, pf.p, pf.len);
+    else if (out) {
+        set_err("output buffer too small");
+        rc = 1;
+    }
+    free(pf.p), free(z), free(pt), free(tau), free(az), free(bz), free(cz), free(evals), free(r_x), free(r_y);
+    free(sc.rand), free(s2.rand);
+    for (int m = 0; m < 3; ++m) free(mt[m].val);
+    return rc;
+}

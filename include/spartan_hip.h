@@ -1,0 +1,115 @@
+/* spartan_hip — MI355X-native drop-in for the proving hot path of tsunrise/r1cs-spartan.
+ *
+ * C ABI of libspartan_hip.so. Every entry point returns an spx_status; on failure
+ * spx_last_error() holds a thread-local message. No torch / HIP types cross this boundary:
+ * plain pointers, sizes and byte images.
+ *
+ * Byte conventions (ark-serialize, the reference's own wire format):
+ *   Fr        32-byte little-endian canonical integer (`into_repr` bytes)
+ *   G1 / G2   96 / 192-byte UNCOMPRESSED affine points (public-parameter files),
+ *             48 / 96-byte COMPRESSED points inside proofs
+ *   Matrix    CSR: row_ptr[n+1] (u64), col[nnz] (u32), val[nnz] (Fr bytes); the row order and
+ *             the order of entries inside a row are the `ark_relations::r1cs::Matrix<F>` order
+ *             (they are hashed into the Fiat-Shamir transcript, /root/reference/src/lib.rs:61-64).
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   spx_index            MLArgumentForR1CS::index                 src/lib.rs:45-51 -> src/ahp/indexer.rs:41-64
+ *   spx_prove            MLArgumentForR1CS::prove                 src/lib.rs:58-146
+ *   spx_pp_load          PublicParameter (CanonicalDeserialize)   src/commitment/data_structures.rs:9-17
+ *   spx_pp_generate      MLProofForR1CS::setup / MLPolyCommit::keygen  src/ahp/setup.rs:13-16, src/commitment/setup.rs:27-105
+ *   spx_commit           MLPolyCommit::commit                     src/commitment/commit.rs:17-29
+ *   spx_open             MLPolyCommit::open                       src/commitment/open.rs:19-58
+ *   spx_sum_over_y       MatrixExtension::sum_over_y              src/data_structures/r1cs_reader.rs:75-85
+ *   spx_eval_on_x        MatrixExtension::eval_on_x               src/data_structures/r1cs_reader.rs:91-117
+ *   spx_msm_g1 / _g2     ark-ec VariableBaseMSM::multi_scalar_mul (called at commit.rs:25, open.rs:49)
+ * Errors mirror src/error.rs:5-14 (Display is todo!() there; here a message string).
+ */
+#ifndef SPARTAN_HIP_H
+#define SPARTAN_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SPX_OK = 0,
+    SPX_INVALID_ARGUMENT = 1, /* Error::InvalidArgument */
+    SPX_SUMCHECK = 2,         /* Error::SumCheckError */
+    SPX_WRONG_WITNESS = 3,    /* Error::WrongWitness */
+    SPX_SERIALIZATION = 4,    /* Error::SerializationError */
+    SPX_DEVICE = 5            /* HIP / RCCL failure (no reference counterpart) */
+} spx_status;
+
+typedef struct spx_ctx spx_ctx;         /* one GPU (one rank): stream, workspaces, communicator */
+typedef struct spx_pp spx_pp;           /* device-resident public parameters (+ window tables) */
+typedef struct spx_pk spx_pk;           /* prover key (IndexPK): matrices on host (transcript) and device */
+typedef struct spx_witness spx_witness; /* z = v || w resident in HBM */
+
+typedef struct {
+    uint64_t n;               /* rows (= number of constraints) */
+    const uint64_t *row_ptr;  /* n + 1 */
+    const uint32_t *col;      /* nnz */
+    const uint8_t *val;       /* 32 * nnz */
+} spx_csr;
+
+typedef enum { SPX_FS = 0, SPX_INJECTED = 1 } spx_mode;
+
+typedef struct {
+    int mode;            /* SPX_FS: Blake2s512Rng Fiat-Shamir (reference); SPX_INJECTED: SplitMix64(inj_seed) */
+    uint64_t inj_seed;
+    int cached_matrix_transcript; /* 1: resume the Blake2s state absorbed at spx_index time (bit-identical) */
+} spx_prove_opts;
+
+const char *spx_last_error(void);
+const char *spx_version(void);
+
+/* ---- context / multi-GPU ---- */
+int spx_ctx_create(int device, spx_ctx **out);
+int spx_ctx_destroy(spx_ctx *ctx);
+/* RCCL (one process per GPU): rank 0 calls spx_comm_unique_id, broadcasts the 128 bytes out of band
+ * (e.g. torch.distributed), then every rank calls spx_ctx_set_comm_rccl. */
+int spx_comm_unique_id(uint8_t id_out[128]);
+int spx_ctx_set_comm_rccl(spx_ctx *ctx, const uint8_t id[128], int rank, int world);
+/* In-process test communicator: `world` contexts sharing one exchange object (shards of one proof
+ * driven by `world` host threads). group_create returns a handle; each ctx joins with its rank. */
+int spx_comm_group_create(int world, void **group_out);
+int spx_comm_group_destroy(void *group);
+int spx_ctx_set_comm_group(spx_ctx *ctx, void *group, int rank);
+
+/* ---- public parameters ---- */
+int spx_pp_load(spx_ctx *ctx, const uint8_t *bytes, size_t len, spx_pp **out);
+int spx_pp_generate(spx_ctx *ctx, int nv, uint64_t seed, spx_pp **out);
+int spx_pp_serialize(spx_pp *pp, uint8_t *out, size_t cap, size_t *len);
+int spx_pp_free(spx_pp *pp);
+
+/* ---- index / witness / prove ---- */
+int spx_index(spx_ctx *ctx, const spx_csr *a, const spx_csr *b, const spx_csr *c, spx_pk **out);
+int spx_index_free(spx_pk *idx);
+int spx_witness_upload(spx_ctx *ctx, const uint8_t *v, size_t nv, const uint8_t *w, size_t nw, spx_witness **out);
+int spx_witness_free(spx_witness *wit);
+size_t spx_proof_size(int log_n, int log_v);
+/* host buffers in, proof bytes out (the reference's prove(pk, v, w, &pp) -> Proof, serialized) */
+int spx_prove(spx_ctx *ctx, spx_pk *idx, const uint8_t *v, size_t nv, const uint8_t *w, size_t nw, spx_pp *pp,
+              const spx_prove_opts *opts, uint8_t *out, size_t cap, size_t *len);
+/* witness already resident in HBM (the benchmarked form) */
+int spx_prove_witness(spx_ctx *ctx, spx_pk *idx, spx_witness *wit, spx_pp *pp, const spx_prove_opts *opts,
+                      uint8_t *out, size_t cap, size_t *len);
+/* per-phase device timings of the last prove on this ctx, microseconds */
+int spx_last_timings(spx_ctx *ctx, double *out, int cap, int *n);
+
+/* ---- kernel-level entry points (parity tests) ---- */
+int spx_sum_over_y(spx_ctx *ctx, const spx_csr *m, const uint8_t *z, uint8_t *out);
+int spx_eval_on_x(spx_ctx *ctx, const spx_csr *m, const uint8_t *r_x, uint8_t *out);
+int spx_msm_g1(spx_ctx *ctx, const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out96);
+int spx_msm_g2(spx_ctx *ctx, const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out192);
+int spx_commit(spx_ctx *ctx, spx_pp *pp, const uint8_t *table, int nv, uint8_t *out56);
+/* proof_out: Proof{h, proofs} compressed = 96 + 8 + 96 * nv bytes */
+int spx_open(spx_ctx *ctx, spx_pp *pp, const uint8_t *table, int nv, const uint8_t *point, uint8_t *eval_out,
+             uint8_t *proof_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

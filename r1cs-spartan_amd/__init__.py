@@ -1,0 +1,406 @@
+"""r1cs-spartan_amd — MI355X-native drop-in for the proving hot path of tsunrise/r1cs-spartan.
+
+Host-side mirror of the reference interface over the C ABI of libspartan_hip.so
+(include/spartan_hip.h). Names, argument meaning and errors follow the reference:
+
+  MLArgumentForR1CS.index(A, B, C) -> IndexPK          /root/reference/src/lib.rs:45-51
+  MLArgumentForR1CS.prove(pk, v, w, pp) -> bytes       /root/reference/src/lib.rs:58-146
+  MLProofForR1CS.setup(nv, seed) -> PublicParameter    /root/reference/src/ahp/setup.rs:13-16
+  MLPolyCommit.commit / open                           /root/reference/src/commitment/{commit,open}.rs
+  MatrixExtension.sum_over_y / eval_on_x               /root/reference/src/data_structures/r1cs_reader.rs
+  InvalidArgument / SumCheckError / WrongWitness / SerializationError   src/error.rs:5-14
+
+The product path is the HIP library only: importing this module loads libspartan_hip.so and
+raises if it is missing; there is no CPU fallback. Field elements are Python ints (canonical) or
+32-byte little-endian canonical byte strings; matrices are `Matrix<F>` = list of rows of
+(coeff, col) or a `Csr` (row_ptr / col / val bytes).
+
+The directory name contains a hyphen, so load it with importlib (see __graft_entry__.py):
+    spec = importlib.util.spec_from_file_location("r1cs_spartan_amd", ".../__init__.py")
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspartan_hip.so")
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+class SpartanError(Exception):
+    code = -1
+
+
+class InvalidArgument(SpartanError):
+    code = 1
+
+
+class SumCheckError(SpartanError):
+    code = 2
+
+
+class WrongWitness(SpartanError):
+    code = 3
+
+
+class SerializationError(SpartanError):
+    code = 4
+
+
+class DeviceError(SpartanError):
+    code = 5
+
+
+_ERRORS = {1: InvalidArgument, 2: SumCheckError, 3: WrongWitness, 4: SerializationError, 5: DeviceError}
+
+
+class _CCsr(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("row_ptr", ctypes.POINTER(ctypes.c_uint64)),
+        ("col", ctypes.POINTER(ctypes.c_uint32)),
+        ("val", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("inj_seed", ctypes.c_uint64), ("cached_matrix_transcript", ctypes.c_int)]
+
+
+EXPORTED = [
+    "spx_last_error",
+    "spx_version",
+    "spx_ctx_create",
+    "spx_ctx_destroy",
+    "spx_comm_unique_id",
+    "spx_ctx_set_comm_rccl",
+    "spx_comm_group_create",
+    "spx_comm_group_destroy",
+    "spx_ctx_set_comm_group",
+    "spx_pp_load",
+    "spx_pp_generate",
+    "spx_pp_serialize",
+    "spx_pp_free",
+    "spx_index",
+    "spx_index_free",
+    "spx_witness_upload",
+    "spx_witness_free",
+    "spx_proof_size",
+    "spx_prove",
+    "spx_prove_witness",
+    "spx_last_timings",
+    "spx_sum_over_y",
+    "spx_eval_on_x",
+    "spx_msm_g1",
+    "spx_msm_g2",
+    "spx_commit",
+    "spx_open",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libspartan_hip.so (fails loudly: the HIP path is the only product path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libspartan_hip.so not built (run __graft_entry__.build()): %s" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    u8p = ctypes.c_char_p
+    L.spx_last_error.restype = ctypes.c_char_p
+    L.spx_version.restype = ctypes.c_char_p
+    L.spx_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_ctx_destroy.argtypes = [vp]
+    L.spx_comm_unique_id.argtypes = [ctypes.c_void_p]
+    L.spx_ctx_set_comm_rccl.argtypes = [vp, u8p, ctypes.c_int, ctypes.c_int]
+    L.spx_comm_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_comm_group_destroy.argtypes = [vp]
+    L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
+    L.spx_pp_load.argtypes = [vp, u8p, sz, ctypes.POINTER(vp)]
+    L.spx_pp_generate.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.spx_pp_serialize.argtypes = [vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_pp_free.argtypes = [vp]
+    L.spx_index.argtypes = [vp, ctypes.POINTER(_CCsr), ctypes.POINTER(_CCsr), ctypes.POINTER(_CCsr), ctypes.POINTER(vp)]
+    L.spx_index_free.argtypes = [vp]
+    L.spx_witness_upload.argtypes = [vp, u8p, sz, u8p, sz, ctypes.POINTER(vp)]
+    L.spx_witness_free.argtypes = [vp]
+    L.spx_proof_size.restype = sz
+    L.spx_proof_size.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.spx_prove.argtypes = [vp, vp, u8p, sz, u8p, sz, vp, ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_prove_witness.argtypes = [vp, vp, vp, vp, ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.spx_sum_over_y.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
+    L.spx_eval_on_x.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
+    L.spx_msm_g1.argtypes = [vp, u8p, u8p, sz, ctypes.c_void_p]
+    L.spx_msm_g2.argtypes = [vp, u8p, u8p, sz, ctypes.c_void_p]
+    L.spx_commit.argtypes = [vp, vp, u8p, ctypes.c_int, ctypes.c_void_p]
+    L.spx_open.argtypes = [vp, vp, u8p, ctypes.c_int, u8p, ctypes.c_void_p, ctypes.c_void_p]
+    for name in EXPORTED:
+        if name not in ("spx_last_error", "spx_version", "spx_proof_size"):
+            getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().spx_last_error().decode(errors="replace")
+        raise _ERRORS.get(rc, SpartanError)(msg)
+
+
+# ------------------------------------------------------------------ data helpers
+def fr_bytes(values):
+    """Canonical ints -> concatenated 32-byte LE images."""
+    return b"".join((int(x) % R).to_bytes(32, "little") for x in values)
+
+
+def fr_ints(b):
+    return [int.from_bytes(b[32 * i : 32 * i + 32], "little") for i in range(len(b) // 32)]
+
+
+class Csr:
+    """CSR image of an ark-relations `Matrix<F>` (row order and in-row order preserved)."""
+
+    def __init__(self, n, row_ptr, col, val_bytes):
+        self.n = int(n)
+        self.row_ptr = row_ptr if isinstance(row_ptr, ctypes.Array) else (ctypes.c_uint64 * (self.n + 1))(*row_ptr)
+        nnz = int(self.row_ptr[self.n])
+        self.col = col if isinstance(col, ctypes.Array) else (ctypes.c_uint32 * max(nnz, 1))(*col)
+        self.val = val_bytes if isinstance(val_bytes, ctypes.Array) else ctypes.create_string_buffer(bytes(val_bytes), max(len(val_bytes), 1))
+        self.nnz = nnz
+
+    @staticmethod
+    def from_rows(rows):
+        rp, col, val = [0], [], bytearray()
+        for row in rows:
+            for coeff, c in row:
+                col.append(int(c))
+                val += (int(coeff) % R).to_bytes(32, "little")
+            rp.append(len(col))
+        return Csr(len(rows), rp, col, bytes(val))
+
+    def c(self):
+        return _CCsr(self.n, self.row_ptr, self.col, ctypes.cast(self.val, ctypes.POINTER(ctypes.c_uint8)))
+
+
+def _as_csr(m):
+    return m if isinstance(m, Csr) else Csr.from_rows(m)
+
+
+def _as_bytes(v):
+    if isinstance(v, (bytes, bytearray)):
+        return bytes(v)
+    return fr_bytes(v)
+
+
+# ------------------------------------------------------------------ handles
+class Context:
+    """One GPU (one rank). Everything else is created against a context."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().spx_ctx_create(int(device), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().spx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_comm_rccl(self, unique_id, rank, world):
+        _check(lib().spx_ctx_set_comm_rccl(self.h, bytes(unique_id), int(rank), int(world)))
+
+    def set_comm_group(self, group, rank):
+        _check(lib().spx_ctx_set_comm_group(self.h, group.h, int(rank)))
+
+    def last_timings(self):
+        buf = (ctypes.c_double * 32)()
+        n = ctypes.c_int(0)
+        _check(lib().spx_last_timings(self.h, buf, 32, ctypes.byref(n)))
+        names = ["transcript_matrices", "commit", "open_rv", "sumcheck1", "eval_on_x", "sumcheck2", "open_ry", "total"]
+        return {names[i] if i < len(names) else str(i): buf[i] for i in range(min(n.value, 32))}
+
+
+class CommGroup:
+    """In-process communicator for `world` contexts (tests of the sharded path on one node)."""
+
+    def __init__(self, world):
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_group_create(int(world), ctypes.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().spx_comm_group_destroy(self.h)
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().spx_comm_unique_id(buf))
+    return buf.raw
+
+
+class PublicParameter:
+    """commitment/data_structures.rs:9-17, resident in HBM with its window tables."""
+
+    def __init__(self, ctx, h, nv):
+        self.ctx, self.h, self.nv = ctx, h, nv
+
+    @staticmethod
+    def load(ctx, data):
+        h = ctypes.c_void_p()
+        _check(lib().spx_pp_load(ctx.h, bytes(data), len(data), ctypes.byref(h)))
+        return PublicParameter(ctx, h, int.from_bytes(data[:8], "little"))
+
+    def serialize_uncompressed(self):
+        n = ctypes.c_size_t(0)
+        _check(lib().spx_pp_serialize(self.h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        _check(lib().spx_pp_serialize(self.h, buf, n.value, ctypes.byref(n)))
+        return buf.raw
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().spx_pp_free(self.h)
+        except Exception:
+            pass
+
+
+class IndexPK:
+    """ahp/indexer.rs:9-17 (prover key)."""
+
+    def __init__(self, ctx, h, log_n):
+        self.ctx, self.h, self.log_n = ctx, h, log_n
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().spx_index_free(self.h)
+        except Exception:
+            pass
+
+
+class Witness:
+    """z = v || w resident in HBM (the benchmarked form of prove's input)."""
+
+    def __init__(self, ctx, v, w):
+        vb, wb = _as_bytes(v), _as_bytes(w)
+        h = ctypes.c_void_p()
+        _check(lib().spx_witness_upload(ctx.h, vb, len(vb) // 32, wb, len(wb) // 32, ctypes.byref(h)))
+        self.ctx, self.h = ctx, h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().spx_witness_free(self.h)
+        except Exception:
+            pass
+
+
+def _opts(mode, seed, cached):
+    return _Opts(1 if mode == "injected" else 0, int(seed), 1 if cached else 0)
+
+
+class MLProofForR1CS:
+    @staticmethod
+    def setup(ctx, nv, seed):
+        """GPU keygen with setup.rs semantics; draws (g, h, t) from SplitMix64(seed)."""
+        h = ctypes.c_void_p()
+        _check(lib().spx_pp_generate(ctx.h, int(nv), int(seed), ctypes.byref(h)))
+        return PublicParameter(ctx, h, nv)
+
+
+class MLArgumentForR1CS:
+    @staticmethod
+    def index(ctx, matrix_a, matrix_b, matrix_c):
+        A, B, C = (_as_csr(m) for m in (matrix_a, matrix_b, matrix_c))
+        h = ctypes.c_void_p()
+        ca, cb, cc = A.c(), B.c(), C.c()
+        _check(lib().spx_index(ctx.h, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(cc), ctypes.byref(h)))
+        return IndexPK(ctx, h, A.n.bit_length() - 1)
+
+    @staticmethod
+    def prove(pk, v, w, pp, mode="fs", seed=0, cached=False):
+        """Proof bytes (ark-serialize compressed, proof.rs:10-20 field order)."""
+        vb, wb = _as_bytes(v), _as_bytes(w)
+        cap = lib().spx_proof_size(pk.log_n, 0)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        o = _opts(mode, seed, cached)
+        _check(lib().spx_prove(pk.ctx.h, pk.h, vb, len(vb) // 32, wb, len(wb) // 32, pp.h, ctypes.byref(o), out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    @staticmethod
+    def prove_witness(pk, wit, pp, mode="fs", seed=0, cached=False):
+        cap = lib().spx_proof_size(pk.log_n, 0)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        o = _opts(mode, seed, cached)
+        _check(lib().spx_prove_witness(pk.ctx.h, pk.h, wit.h, pp.h, ctypes.byref(o), out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+
+class MatrixExtension:
+    @staticmethod
+    def sum_over_y(ctx, matrix, z):
+        M = _as_csr(matrix)
+        zb = _as_bytes(z)
+        out = ctypes.create_string_buffer(32 * M.n)
+        c = M.c()
+        _check(lib().spx_sum_over_y(ctx.h, ctypes.byref(c), zb, out))
+        return out.raw
+
+    @staticmethod
+    def eval_on_x(ctx, matrix, r_x):
+        M = _as_csr(matrix)
+        rb = _as_bytes(r_x)
+        out = ctypes.create_string_buffer(32 * M.n)
+        c = M.c()
+        _check(lib().spx_eval_on_x(ctx.h, ctypes.byref(c), rb, out))
+        return out.raw
+
+
+class MLPolyCommit:
+    @staticmethod
+    def commit(pp, table):
+        tb = _as_bytes(table)
+        out = ctypes.create_string_buffer(56)
+        _check(lib().spx_commit(pp.ctx.h, pp.h, tb, (len(tb) // 32).bit_length() - 1, out))
+        return out.raw
+
+    @staticmethod
+    def open(pp, table, point):
+        tb, pb = _as_bytes(table), _as_bytes(point)
+        nv = len(pb) // 32
+        ev = ctypes.create_string_buffer(32)
+        pf = ctypes.create_string_buffer(96 + 8 + 96 * nv)
+        _check(lib().spx_open(pp.ctx.h, pp.h, tb, nv, pb, ev, pf))
+        return ev.raw, pf.raw
+
+
+def msm_g1(ctx, bases_uncompressed, scalars):
+    sb = _as_bytes(scalars)
+    out = ctypes.create_string_buffer(96)
+    _check(lib().spx_msm_g1(ctx.h, bytes(bases_uncompressed), sb, len(sb) // 32, out))
+    return out.raw
+
+
+def msm_g2(ctx, bases_uncompressed, scalars):
+    sb = _as_bytes(scalars)
+    out = ctypes.create_string_buffer(192)
+    _check(lib().spx_msm_g2(ctx.h, bytes(bases_uncompressed), sb, len(sb) // 32, out))
+    return out.raw

@@ -1,0 +1,253 @@
+// extern "C" boundary (include/spartan_hip.h). Exceptions never cross it: every entry point
+// maps them to an spx_status and a thread-local message (the reference's Error::Display is
+// todo!(), /root/reference/src/error.rs:23-27).
+#include "../../include/spartan_hip.h"
+
+#include <memory>
+#include <string>
+
+#include "prover.hpp"
+
+extern "C" int spx_comm_unique_id_impl(uint8_t out[128]);
+
+struct spx_ctx {
+    std::unique_ptr<spx::Ctx> c;
+};
+struct spx_pp {
+    spx_ctx* ctx;
+    std::unique_ptr<spx::PP> p;
+};
+struct spx_pk {
+    spx_ctx* ctx;
+    std::unique_ptr<spx::Index> i;
+};
+struct spx_witness {
+    spx_ctx* ctx;
+    std::unique_ptr<spx::Witness> w;
+};
+
+namespace {
+thread_local std::string g_err;
+template <class F>
+int guard(F&& f) {
+    try {
+        f();
+        g_err.clear();
+        return SPX_OK;
+    } catch (const spx::SpxError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of memory";
+        return SPX_DEVICE;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SPX_DEVICE;
+    }
+}
+spx::HostCsr to_host(const spx_csr* m) {
+    if (!m || !m->row_ptr) spx::invalid("null matrix");
+    spx::HostCsr h;
+    h.n = m->n;
+    h.rp.assign(m->row_ptr, m->row_ptr + m->n + 1);
+    const uint64_t nnz = h.rp[m->n];
+    if (nnz && (!m->col || !m->val)) spx::invalid("null matrix arrays");
+    h.col.assign(m->col, m->col + nnz);
+    h.val.assign(m->val, m->val + 32 * nnz);
+    return h;
+}
+void set_dev(spx_ctx* c) {
+    if (!c) spx::invalid("null context");
+    SPX_HIP(hipSetDevice(c->c->device));
+}
+spx::ProveOpts opts_of(const spx_prove_opts* o) {
+    spx::ProveOpts p;
+    if (o) {
+        if (o->mode != SPX_FS && o->mode != SPX_INJECTED) spx::invalid("bad mode");
+        p.mode = o->mode;
+        p.seed = o->inj_seed;
+        p.cached = o->cached_matrix_transcript != 0;
+    }
+    return p;
+}
+int copy_out(const std::vector<uint8_t>& v, uint8_t* out, size_t cap, size_t* len) {
+    if (len) *len = v.size();
+    if (out) {
+        if (cap < v.size()) spx::invalid("output buffer too small");
+        memcpy(out, v.data(), v.size());
+    }
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+const char* spx_last_error(void) { return g_err.c_str(); }
+const char* spx_version(void) { return "spartan_hip 0.1 (gfx950)"; }
+
+int spx_ctx_create(int device, spx_ctx** out) {
+    return guard([&] {
+        if (!out) spx::invalid("null out");
+        int ndev = 0;
+        SPX_HIP(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) spx::invalid("no such HIP device");
+        auto* c = new spx_ctx();
+        c->c.reset(new spx::Ctx(device));
+        *out = c;
+    });
+}
+int spx_ctx_destroy(spx_ctx* ctx) {
+    return guard([&] { delete ctx; });
+}
+int spx_comm_unique_id(uint8_t id_out[128]) {
+    return guard([&] {
+        if (spx_comm_unique_id_impl(id_out)) throw spx::SpxError(spx::kDevice, "ncclGetUniqueId failed");
+    });
+}
+int spx_ctx_set_comm_rccl(spx_ctx* ctx, const uint8_t id[128], int rank, int world) {
+    return guard([&] {
+        set_dev(ctx);
+        if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
+        ctx->c->comm = spx::make_rccl_comm(id, rank, world, ctx->c->device, ctx->c->stream);
+    });
+}
+int spx_comm_group_create(int world, void** group_out) {
+    return guard([&] {
+        if (world < 1) spx::invalid("bad world");
+        *group_out = new std::shared_ptr<spx::GroupState>(std::make_shared<spx::GroupState>(world));
+    });
+}
+int spx_comm_group_destroy(void* group) {
+    return guard([&] { delete static_cast<std::shared_ptr<spx::GroupState>*>(group); });
+}
+int spx_ctx_set_comm_group(spx_ctx* ctx, void* group, int rank) {
+    return guard([&] {
+        auto& st = *static_cast<std::shared_ptr<spx::GroupState>*>(group);
+        if (rank < 0 || rank >= st->world) spx::invalid("bad rank");
+        ctx->c->comm.reset(new spx::GroupComm(st, rank));
+    });
+}
+
+int spx_pp_load(spx_ctx* ctx, const uint8_t* bytes, size_t len, spx_pp** out) {
+    return guard([&] {
+        set_dev(ctx);
+        auto* p = new spx_pp{ctx, spx::pp_load(*ctx->c, bytes, len)};
+        *out = p;
+    });
+}
+int spx_pp_generate(spx_ctx* ctx, int nv, uint64_t seed, spx_pp** out) {
+    return guard([&] {
+        set_dev(ctx);
+        auto* p = new spx_pp{ctx, spx::pp_generate(*ctx->c, nv, seed)};
+        *out = p;
+    });
+}
+int spx_pp_serialize(spx_pp* pp, uint8_t* out, size_t cap, size_t* len) {
+    return guard([&] {
+        set_dev(pp->ctx);
+        copy_out(spx::pp_serialize(*pp->ctx->c, *pp->p), out, cap, len);
+    });
+}
+int spx_pp_free(spx_pp* pp) {
+    return guard([&] {
+        if (pp) set_dev(pp->ctx);
+        delete pp;
+    });
+}
+
+int spx_index(spx_ctx* ctx, const spx_csr* a, const spx_csr* b, const spx_csr* c, spx_pk** out) {
+    return guard([&] {
+        set_dev(ctx);
+        spx::HostCsr m[3] = {to_host(a), to_host(b), to_host(c)};
+        *out = new spx_pk{ctx, spx::index_build(*ctx->c, m)};
+    });
+}
+int spx_index_free(spx_pk* idx) {
+    return guard([&] {
+        if (idx) set_dev(idx->ctx);
+        delete idx;
+    });
+}
+int spx_witness_upload(spx_ctx* ctx, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw, spx_witness** out) {
+    return guard([&] {
+        set_dev(ctx);
+        *out = new spx_witness{ctx, spx::witness_upload(*ctx->c, v, nv, w, nw)};
+    });
+}
+int spx_witness_free(spx_witness* wit) {
+    return guard([&] {
+        if (wit) set_dev(wit->ctx);
+        delete wit;
+    });
+}
+size_t spx_proof_size(int log_n, int /*log_v*/) { return spx::proof_size(log_n); }
+
+int spx_prove(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw, spx_pp* pp,
+              const spx_prove_opts* opts, uint8_t* out, size_t cap, size_t* len) {
+    return guard([&] {
+        set_dev(ctx);
+        auto W = spx::witness_upload(*ctx->c, v, nv, w, nw);
+        copy_out(spx::prove(*ctx->c, *idx->i, *W, *pp->p, opts_of(opts)), out, cap, len);
+    });
+}
+int spx_prove_witness(spx_ctx* ctx, spx_pk* idx, spx_witness* wit, spx_pp* pp, const spx_prove_opts* opts,
+                      uint8_t* out, size_t cap, size_t* len) {
+    return guard([&] {
+        set_dev(ctx);
+        copy_out(spx::prove(*ctx->c, *idx->i, *wit->w, *pp->p, opts_of(opts)), out, cap, len);
+    });
+}
+int spx_last_timings(spx_ctx* ctx, double* out, int cap, int* n) {
+    return guard([&] {
+        auto& t = ctx->c->timings;
+        if (n) *n = (int)t.size();
+        for (int i = 0; i < (int)t.size() && i < cap; ++i) out[i] = t[i].second;
+    });
+}
+
+int spx_sum_over_y(spx_ctx* ctx, const spx_csr* m, const uint8_t* z, uint8_t* out) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_sum_over_y(*ctx->c, to_host(m), z);
+        memcpy(out, r.data(), r.size());
+    });
+}
+int spx_eval_on_x(spx_ctx* ctx, const spx_csr* m, const uint8_t* r_x, uint8_t* out) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_eval_on_x(*ctx->c, to_host(m), r_x);
+        memcpy(out, r.data(), r.size());
+    });
+}
+int spx_msm_g1(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out96) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_msm(*ctx->c, false, bases, scalars, n);
+        memcpy(out96, r.data(), r.size());
+    });
+}
+int spx_msm_g2(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out192) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_msm(*ctx->c, true, bases, scalars, n);
+        memcpy(out192, r.data(), r.size());
+    });
+}
+int spx_commit(spx_ctx* ctx, spx_pp* pp, const uint8_t* table, int nv, uint8_t* out56) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_commit(*ctx->c, *pp->p, table, nv);
+        memcpy(out56, r.data(), r.size());
+    });
+}
+int spx_open(spx_ctx* ctx, spx_pp* pp, const uint8_t* table, int nv, const uint8_t* point, uint8_t* eval_out,
+             uint8_t* proof_out) {
+    return guard([&] {
+        set_dev(ctx);
+        auto r = spx::k_open(*ctx->c, *pp->p, table, nv, point);
+        memcpy(eval_out, r.data(), 32);
+        memcpy(proof_out, r.data() + 32, r.size() - 32);
+    });
+}
+
+}  // extern "C"

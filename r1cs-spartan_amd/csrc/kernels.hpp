@@ -1,0 +1,91 @@
+// Kernel-launch interface shared by the device translation units and the host prover.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "curve_dev.hpp"
+
+namespace spx {
+
+// rows longer than this go to the chunked long-row path (nnz skew, e.g. the dense row of
+// the reference's TestSynthesizer at density 0, constraints.rs:77-88)
+static constexpr uint64_t kLongRow = 64;
+static constexpr uint64_t kChunk = 4096;
+
+struct SparseView3 {            // three CSR (or CSC) matrices, local index space
+    const uint64_t* ptr[3];     // [count + 1]
+    const uint32_t* idx[3];     // column (CSR) / row (CSC) indices, global
+    const Fr* val[3];           // Montgomery values
+};
+struct LongChunk {
+    uint32_t m;
+    uint32_t pad;
+    uint64_t begin, end;
+};
+struct LongRow {
+    uint32_t m;
+    uint32_t chunk_begin, chunk_end;
+    uint32_t pad;
+    uint64_t x;  // local output index
+};
+struct Tables3 {
+    Fr* t[3];
+};
+
+// ---- mle_kernels.hip
+void launch_to_mont(Fr* d, size_t n, int* err, hipStream_t s);
+void launch_from_mont(Fr* out, const Fr* in, size_t n, hipStream_t s);
+void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* o1, Fr* o2, const Fr* scale,
+                    uint64_t count, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
+                    Fr* partial, hipStream_t s);
+void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
+                     Fr* scratch_hi, hipStream_t s);
+int sc_grid(uint64_t half);
+void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr* r,
+                      uint64_t half, Fr* partial, Fr* result3, hipStream_t s);
+void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr* r, uint64_t half,
+                      Fr* partial, Fr* result3, hipStream_t s);
+void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s);
+
+// ---- msm.hip
+// One MSM inside a batch. Bases are the PRECOMPUTED window copies of a base set:
+// pts[pts_off + w * stride + j] = 2^(c w) * B_j (affine), so every window shares one bucket set.
+struct MsmInst {
+    uint64_t pts_off;     // first precomputed point of this base set
+    uint64_t scalar_off;  // first scalar (Montgomery Fr) in the batch scalar array
+    uint32_t size;        // number of (base, scalar) pairs
+    uint32_t c, W;        // window bits, windows
+    uint32_t bucket_off;  // first bucket of this instance (2^(c-1) buckets)
+    uint32_t red_off;     // first bucket-reduction slot
+    uint32_t red_T, red_L;  // reduction threads and buckets per thread
+    uint32_t stride;      // points per window copy of the base set (>= size; local blocks)
+};
+
+struct MsmWorkspace;  // opaque, owned by the host side (msm.hip)
+MsmWorkspace* msm_ws_create();
+void msm_ws_destroy(MsmWorkspace* ws);
+
+// Runs a batch of MSMs on `s`; out_xyzz receives one XYZZ point per instance (G1: 4 x 48 B,
+// G2: 4 x 96 B, Montgomery limbs). Synchronises once on `s` to size the accumulation levels.
+void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G1Aff* pts, const Fr* scalars,
+                void* out_xyzz_dev, hipStream_t s);
+void msm_run_g2(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G2Aff* pts, const Fr* scalars,
+                void* out_xyzz_dev, hipStream_t s);
+
+// PP preprocessing: for each base B_j (raw affine, level array), write the W window copies
+// 2^(c w) B_j (affine) to dst[w * count + j]. pair_sum: B_j := raw[2j] + raw[2j+1].
+void precompute_windows_g1(const G1Aff* raw, uint64_t count, bool pair_sum, int c, int W, G1Aff* dst, void* tmp,
+                           hipStream_t s);
+void precompute_windows_g2(const G2Aff* raw, uint64_t count, bool pair_sum, int c, int W, G2Aff* dst, void* tmp,
+                           hipStream_t s);
+// raw ark-serialize uncompressed points (canonical, flags) -> device affine Montgomery, in place.
+// Infinity (flag bit 6) becomes the (0,0) sentinel. err |= 1 on malformed input.
+void launch_points_from_bytes_g1(G1Aff* pts, uint64_t n, int* err, hipStream_t s);
+void launch_points_from_bytes_g2(G2Aff* pts, uint64_t n, int* err, hipStream_t s);
+void launch_points_to_canon_g1(G1Aff* pts, uint64_t n, hipStream_t s);
+void launch_points_to_canon_g2(G2Aff* pts, uint64_t n, hipStream_t s);
+// keygen: out[i] = scalar_i * base, with table[w * 256 + d] = d * 2^(8 w) * base (affine, 32 windows)
+void fixed_base_g1(const G1Aff* table, const Fr* scalars, uint64_t n, G1Aff* out, void* tmp, hipStream_t s);
+void fixed_base_g2(const G2Aff* table, const Fr* scalars, uint64_t n, G2Aff* out, void* tmp, hipStream_t s);
+
+}  // namespace spx

@@ -1,0 +1,422 @@
+// HBM-streaming Fr kernels of the hot path:
+//   * canonical <-> Montgomery conversion of witness / matrix values,
+//   * sum_over_y  = three CSR SpMVs Az, Bz, Cz (r1cs_reader.rs:75-85),
+//   * eval_on_x   = A(r_x, .) as a CSC gather against eq(r_x), combined over A,B,C with the
+//                   verifier's r_A, r_B, r_C (r1cs_reader.rs:91-117 + prover.rs:239-245),
+//   * eq tables   (eq.rs:5-20 in product form),
+//   * sumcheck rounds (AHPForMLSumcheck::prove_round [upstream]) fused with the binding of the
+//     previous challenge, and the mKZG quotient/fold levels of open.rs:37-45.
+// Every kernel is a grid-stride stream over 32-byte Fr elements (two 16-byte loads per element),
+// with per-block partial sums reduced by wave64 shuffles + LDS and a second one-block pass:
+// the reduction order is fixed, and field addition is exact, so results are deterministic.
+#include "kernels.hpp"
+
+namespace spx {
+
+static constexpr int kThreads = 256;
+
+DEV Fr ld_fr(const Fr* p) {
+    Fr r;
+    load_vec(r, p);
+    return r;
+}
+DEV void st_fr(Fr* p, const Fr& v) { store_vec(p, v); }
+
+// ------------------------------------------------------------------ block reduction of K Fr values
+template <int K>
+DEV void block_reduce_store(Fr (&acc)[K], Fr* out /* K entries for this block */) {
+    __shared__ Fr lds[K][kThreads / 64];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Fr o = shfl_xor(acc[k], m);
+            fe_add(acc[k], acc[k], o);
+        }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[k][wid] = acc[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Fr s = lds[k][0];
+            for (int w = 1; w < (int)(blockDim.x / 64); ++w) fe_add(s, s, lds[k][w]);
+            st_fr(out + k, s);
+        }
+    }
+}
+
+// out[k] = sum over blocks of partial[b*K + k]  (one block)
+template <int K>
+__global__ __launch_bounds__(kThreads) void k_reduce_partials(const Fr* __restrict__ partial, int nblk,
+                                                              Fr* __restrict__ out) {
+    Fr acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) fe_zero(acc[k]);
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) fe_add(acc[k], acc[k], ld_fr(partial + (size_t)b * K + k));
+    }
+    block_reduce_store<K>(acc, out);
+}
+
+// ------------------------------------------------------------------ conversions
+__global__ void k_to_mont(Fr* __restrict__ data, size_t n, int* __restrict__ err) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        Fr c = ld_fr(data + i);
+        if (!fr_is_canonical(c)) atomicOr(err, 1);
+        Fr m;
+        fr_to_mont(m, c);
+        st_fr(data + i, m);
+    }
+}
+__global__ void k_from_mont(Fr* __restrict__ out, const Fr* __restrict__ in, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        Fr m = ld_fr(in + i), c;
+        fe_from_mont(c, m);
+        st_fr(out + i, c);
+    }
+}
+
+// ------------------------------------------------------------------ sparse products
+// Short rows: one thread per output index x (local), three matrices at once. Rows flagged
+// long (row length > kLongRow) contribute nothing here and are added by the chunk kernels.
+// MODE 0 (sum_over_y): out_m[x] = sum_k val_m[k] * vec[col_m[k]] for m = A,B,C.
+// MODE 1 (eval_on_x, combined): out[x] = sum_m scale_m * sum_k val_m[k] * vec[col_m[k]].
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* __restrict__ vec, Fr* out0,
+                                                      Fr* out1, Fr* out2, const Fr* __restrict__ scale,
+                                                      uint64_t count) {
+    Fr s[3];
+    if (MODE == 1) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) s[m] = ld_fr(scale + m);
+    }
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < count;
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        Fr tot;
+        fe_zero(tot);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const uint64_t b = mv.ptr[m][x], e = mv.ptr[m][x + 1];
+            Fr acc;
+            fe_zero(acc);
+            if (e - b <= kLongRow) {
+                for (uint64_t k = b; k < e; ++k) {
+                    Fr v = ld_fr(mv.val[m] + k), zv = ld_fr(vec + mv.idx[m][k]), t;
+                    fe_mul(t, v, zv);
+                    fe_add(acc, acc, t);
+                }
+            }
+            if (MODE == 0) {
+                st_fr(m == 0 ? out0 + x : (m == 1 ? out1 + x : out2 + x), acc);
+            } else {
+                Fr t;
+                fe_mul(t, acc, s[m]);
+                fe_add(tot, tot, t);
+            }
+        }
+        if (MODE == 1) st_fr(out0 + x, tot);
+    }
+}
+
+// Long rows: one block per chunk of <= kChunk entries; partial[chunk] = sum val * vec[idx].
+__global__ __launch_bounds__(kThreads) void k_sparse_chunks(SparseView3 mv, const Fr* __restrict__ vec,
+                                                            const LongChunk* __restrict__ chunks,
+                                                            Fr* __restrict__ partial) {
+    const LongChunk ch = chunks[blockIdx.x];
+    const Fr* val = mv.val[ch.m];
+    const uint32_t* idx = mv.idx[ch.m];
+    Fr acc[1];
+    fe_zero(acc[0]);
+    for (uint64_t k = ch.begin + threadIdx.x; k < ch.end; k += blockDim.x) {
+        Fr v = ld_fr(val + k), zv = ld_fr(vec + idx[k]), t;
+        fe_mul(t, v, zv);
+        fe_add(acc[0], acc[0], t);
+    }
+    block_reduce_store<1>(acc, partial + blockIdx.x);
+}
+
+// Single thread, fixed order: fold the chunk partials of every long (matrix, row) into the outputs.
+template <int MODE>
+__global__ void k_sparse_long_finish(const LongRow* __restrict__ rows, int nrows, const Fr* __restrict__ partial,
+                                     Fr* out0, Fr* out1, Fr* out2, const Fr* __restrict__ scale) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int r = 0; r < nrows; ++r) {
+        const LongRow lr = rows[r];
+        Fr acc;
+        fe_zero(acc);
+        for (uint32_t c = lr.chunk_begin; c < lr.chunk_end; ++c) fe_add(acc, acc, ld_fr(partial + c));
+        Fr* o;
+        if (MODE == 0) {
+            o = (lr.m == 0 ? out0 : (lr.m == 1 ? out1 : out2)) + lr.x;
+        } else {
+            Fr t;
+            fe_mul(t, acc, ld_fr(scale + lr.m));
+            acc = t;
+            o = out0 + lr.x;
+        }
+        Fr cur = ld_fr(o);
+        fe_add(cur, cur, acc);
+        st_fr(o, cur);
+    }
+}
+
+// ------------------------------------------------------------------ eq tables
+// One block: tab[x] = prod_{j<k} eq(r_j, x_j) for x < 2^k (k <= 12), variable 0 = LSB.
+__global__ __launch_bounds__(kThreads) void k_eq_small(const Fr* __restrict__ r, int k, Fr* __restrict__ tab) {
+    if (threadIdx.x == 0) {
+        Fr one;
+        fe_one(one);
+        st_fr(tab, one);
+    }
+    __syncthreads();
+    // step j: tab[x + 2^j] = tab[x] * r_j, tab[x] *= (1 - r_j) for x < 2^j. Each thread touches
+    // only its own x and x + 2^j, so a barrier between steps is the only ordering needed.
+    for (int j = 0; j < k; ++j) {
+        const uint32_t half = 1u << j;
+        Fr rj = ld_fr(r + j), one, om;
+        fe_one(one);
+        fe_sub(om, one, rj);
+        for (uint32_t x = threadIdx.x; x < half; x += blockDim.x) {
+            Fr v = ld_fr(tab + x), a, b;
+            fe_mul(a, v, om);
+            fe_mul(b, v, rj);
+            st_fr(tab + x, a);
+            st_fr(tab + x + half, b);
+        }
+        __syncthreads();
+    }
+}
+
+// out[i] = lo[(i + base) & mask] * hi[(i + base) >> klo],  i < count
+__global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ lo, const Fr* __restrict__ hi, int klo,
+                                                        uint64_t base, uint64_t count, Fr* __restrict__ out) {
+    const uint64_t mask = (1ull << klo) - 1;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = i + base;
+        Fr a = ld_fr(lo + (x & mask)), b = ld_fr(hi + (x >> klo)), t;
+        fe_mul(t, a, b);
+        st_fr(out + i, t);
+    }
+}
+
+// ------------------------------------------------------------------ sumcheck #1 round
+// FOLD == false (round 1): X_t = in[2b + t];            e = E[b]
+// FOLD == true  (round >= 2): X'[2b+u] = in[4b+2u] + r*(in[4b+2u+1] - in[4b+2u]) stored to out,
+//                             e = Ein[2b] + Ein[2b+1] stored to Eout[b]
+// partial[blk] = (G(0), G(1), G(2)) with G(t) = sum_b (A_t B_t - C_t) e,  X_2 = 2 X_1 - X_0.
+template <bool FOLD>
+__global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
+                                                        Fr* __restrict__ Eout, const Fr* __restrict__ rch,
+                                                        uint64_t half, Fr* __restrict__ partial) {
+    Fr r;
+    if (FOLD) r = ld_fr(rch);
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
+        Fr x0[3], x1[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            if (FOLD) {
+                Fr a0 = ld_fr(in.t[m] + 4 * b), a1 = ld_fr(in.t[m] + 4 * b + 1);
+                Fr a2 = ld_fr(in.t[m] + 4 * b + 2), a3 = ld_fr(in.t[m] + 4 * b + 3), d;
+                fe_sub(d, a1, a0);
+                fe_mul(d, d, r);
+                fe_add(x0[m], a0, d);
+                fe_sub(d, a3, a2);
+                fe_mul(d, d, r);
+                fe_add(x1[m], a2, d);
+                st_fr(out.t[m] + 2 * b, x0[m]);
+                st_fr(out.t[m] + 2 * b + 1, x1[m]);
+            } else {
+                x0[m] = ld_fr(in.t[m] + 2 * b);
+                x1[m] = ld_fr(in.t[m] + 2 * b + 1);
+            }
+        }
+        Fr e;
+        if (FOLD) {
+            Fr e0 = ld_fr(Ein + 2 * b), e1 = ld_fr(Ein + 2 * b + 1);
+            fe_add(e, e0, e1);
+            if (Eout) st_fr(Eout + b, e);
+        } else {
+            e = ld_fr(Ein + b);
+        }
+        Fr t, u;
+        // t = 0
+        fe_mul(t, x0[0], x0[1]);
+        fe_sub(t, t, x0[2]);
+        fe_mul(t, t, e);
+        fe_add(g[0], g[0], t);
+        // t = 1
+        fe_mul(t, x1[0], x1[1]);
+        fe_sub(t, t, x1[2]);
+        fe_mul(t, t, e);
+        fe_add(g[1], g[1], t);
+        // t = 2
+        Fr y[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            fe_add(u, x1[m], x1[m]);
+            fe_sub(y[m], u, x0[m]);
+        }
+        fe_mul(t, y[0], y[1]);
+        fe_sub(t, t, y[2]);
+        fe_mul(t, t, e);
+        fe_add(g[2], g[2], t);
+    }
+    block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+
+// ------------------------------------------------------------------ sumcheck #2 round
+// tables M (= sum_m r_m M(r_x, .)) and Z; partial = (P(0), P(1), P(2)), P(t) = sum_b M_t Z_t.
+template <bool FOLD>
+__global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
+                                                        Fr* __restrict__ Mout, Fr* __restrict__ Zout,
+                                                        const Fr* __restrict__ rch, uint64_t half,
+                                                        Fr* __restrict__ partial) {
+    Fr r;
+    if (FOLD) r = ld_fr(rch);
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
+        Fr m0, m1, z0, z1;
+        if (FOLD) {
+            Fr d;
+            Fr a0 = ld_fr(Min + 4 * b), a1 = ld_fr(Min + 4 * b + 1), a2 = ld_fr(Min + 4 * b + 2), a3 = ld_fr(Min + 4 * b + 3);
+            fe_sub(d, a1, a0);
+            fe_mul(d, d, r);
+            fe_add(m0, a0, d);
+            fe_sub(d, a3, a2);
+            fe_mul(d, d, r);
+            fe_add(m1, a2, d);
+            Fr c0 = ld_fr(Zin + 4 * b), c1 = ld_fr(Zin + 4 * b + 1), c2 = ld_fr(Zin + 4 * b + 2), c3 = ld_fr(Zin + 4 * b + 3);
+            fe_sub(d, c1, c0);
+            fe_mul(d, d, r);
+            fe_add(z0, c0, d);
+            fe_sub(d, c3, c2);
+            fe_mul(d, d, r);
+            fe_add(z1, c2, d);
+            st_fr(Mout + 2 * b, m0);
+            st_fr(Mout + 2 * b + 1, m1);
+            st_fr(Zout + 2 * b, z0);
+            st_fr(Zout + 2 * b + 1, z1);
+        } else {
+            m0 = ld_fr(Min + 2 * b);
+            m1 = ld_fr(Min + 2 * b + 1);
+            z0 = ld_fr(Zin + 2 * b);
+            z1 = ld_fr(Zin + 2 * b + 1);
+        }
+        Fr t, u, v;
+        fe_mul(t, m0, z0);
+        fe_add(g[0], g[0], t);
+        fe_mul(t, m1, z1);
+        fe_add(g[1], g[1], t);
+        fe_add(u, m1, m1);
+        fe_sub(u, u, m0);
+        fe_add(v, z1, z1);
+        fe_sub(v, v, z0);
+        fe_mul(t, u, v);
+        fe_add(g[2], g[2], t);
+    }
+    block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+
+// ------------------------------------------------------------------ mKZG open level (open.rs:42-45)
+// q[b] = r[2b+1] - r[2b];  r'[b] = r[2b] + p * q[b]   ( = r[2b](1-p) + r[2b+1] p )
+__global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+                                                         Fr* __restrict__ q, const Fr* __restrict__ point,
+                                                         uint64_t half) {
+    const Fr p = ld_fr(point);
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
+        Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
+        fe_sub(d, a1, a0);
+        st_fr(q + b, d);
+        fe_mul(t, d, p);
+        fe_add(t, a0, t);
+        st_fr(rout + b, t);
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static inline int grid_for(uint64_t n, int cap = 2048) {
+    uint64_t g = (n + kThreads - 1) / kThreads;
+    if (g < 1) g = 1;
+    if (g > (uint64_t)cap) g = cap;
+    return (int)g;
+}
+
+void launch_to_mont(Fr* d, size_t n, int* err, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_to_mont, dim3(grid_for(n, 4096)), dim3(kThreads), 0, s, d, n, err);
+}
+void launch_from_mont(Fr* out, const Fr* in, size_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_from_mont, dim3(grid_for(n, 4096)), dim3(kThreads), 0, s, out, in, n);
+}
+
+void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* o1, Fr* o2, const Fr* scale,
+                    uint64_t count, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
+                    Fr* partial, hipStream_t s) {
+    if (count) {
+        if (mode == 0)
+            hipLaunchKernelGGL(k_sparse3<0>, dim3(grid_for(count, 8192)), dim3(kThreads), 0, s, mv, vec, o0, o1, o2,
+                               scale, count);
+        else
+            hipLaunchKernelGGL(k_sparse3<1>, dim3(grid_for(count, 8192)), dim3(kThreads), 0, s, mv, vec, o0, o1, o2,
+                               scale, count);
+    }
+    if (nchunks > 0) {
+        hipLaunchKernelGGL(k_sparse_chunks, dim3(nchunks), dim3(kThreads), 0, s, mv, vec, chunks, partial);
+        if (mode == 0)
+            hipLaunchKernelGGL(k_sparse_long_finish<0>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, o0, o1, o2,
+                               scale);
+        else
+            hipLaunchKernelGGL(k_sparse_long_finish<1>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, o0, o1, o2,
+                               scale);
+    }
+}
+
+void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
+                     Fr* scratch_hi, hipStream_t s) {
+    // split k = klo + khi, each <= 12 (k <= 24)
+    int klo = (k + 1) / 2, khi = k - klo;
+    hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev, klo, scratch_lo);
+    hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev + klo, khi, scratch_hi);
+    hipLaunchKernelGGL(k_eq_expand, dim3(grid_for(count, 8192)), dim3(kThreads), 0, s, scratch_lo, scratch_hi, klo, base,
+                       count, out);
+}
+
+int sc_grid(uint64_t half) { return grid_for(half, 1024); }
+
+void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr* r,
+                      uint64_t half, Fr* partial, Fr* result3, hipStream_t s) {
+    int g = sc_grid(half);
+    if (fold)
+        hipLaunchKernelGGL(k_sc1_round<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
+    else
+        hipLaunchKernelGGL(k_sc1_round<false>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
+    hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
+}
+
+void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr* r, uint64_t half,
+                      Fr* partial, Fr* result3, hipStream_t s) {
+    int g = sc_grid(half);
+    if (fold)
+        hipLaunchKernelGGL(k_sc2_round<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
+    else
+        hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
+    hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
+}
+
+void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s) {
+    hipLaunchKernelGGL(k_open_level, dim3(grid_for(half, 8192)), dim3(kThreads), 0, s, rin, rout, q, point, half);
+}
+
+}  // namespace spx

@@ -1,0 +1,1150 @@
+// MI355X prover orchestration: the reference's `MLArgumentForR1CS::prove`
+// (/root/reference/src/lib.rs:58-146) with the AHP rounds of src/ahp/prover.rs:109-281 run as
+// HIP kernels (mle_kernels.hip, msm.hip) and the Fiat-Shamir transcript on the host.
+//
+// Sharding: G = 2^g ranks own contiguous blocks of the hypercube (top g bits of x
+// or y). Variables bind LSB first, so every rank folds locally for the first L - g rounds; each
+// round exchanges 3 Fr per rank, each MSM one affine point per rank. The last g rounds/levels run on
+// the gathered G-entry tables. Every rank replays the same transcript, so no challenge broadcast.
+#include "prover.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+namespace spx {
+
+using host::Affine;
+using HFr = host::Fr;
+using HFq = host::Fq;
+using HFq2 = host::Fq2;
+
+// ====================================================================== context
+Ctx::Ctx(int dev) : device(dev) {
+    SPX_HIP(hipSetDevice(dev));
+    SPX_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    msm = msm_ws_create();
+    comm.reset(new LocalComm());
+}
+Ctx::~Ctx() {
+    (void)hipSetDevice(device);
+    msm_ws_destroy(msm);
+    scratch.release();
+    if (pin) (void)hipHostFree(pin);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+uint8_t* Ctx::pinned(size_t b) {
+    if (b > pin_bytes) {
+        if (pin) SPX_HIP(hipHostFree(pin));
+        size_t nb = std::max<size_t>(b, 1 << 16);
+        SPX_HIP(hipHostMalloc((void**)&pin, nb));
+        pin_bytes = nb;
+    }
+    return pin;
+}
+
+static inline int ilog2(uint64_t x) { return 63 - __builtin_clzll(x); }
+static inline bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+// ====================================================================== public parameters
+int window_bits_for(uint64_t size) {
+    int k = size ? ilog2(size) : 0;
+    if (k >= 14) return 16;
+    return std::max(3, k - 2);
+}
+static int windows_for(int c) { return (256 + c - 1) / c; }
+
+template <class A>
+static void precompute_level(Ctx& C, const A* raw, uint64_t count, bool pair, int c, int W, A* dst) {
+    // chunked to bound the XYZZ temporary: tmp XYZZ [W][chunk] -> affine [W][chunk] -> dst rows (pitch count)
+    const uint64_t chunk = std::min<uint64_t>(count, 1ull << 18);
+    const size_t xyzz_sz = 2 * sizeof(A);
+    DevMem tmp(xyzz_sz * chunk * W), aff(sizeof(A) * chunk * W);
+    for (uint64_t j0 = 0; j0 < count; j0 += chunk) {
+        const uint64_t cn = std::min(chunk, count - j0);
+        const A* src = raw + (pair ? 2 * j0 : j0);
+        if constexpr (sizeof(A) == sizeof(G1Aff))
+            precompute_windows_g1((const G1Aff*)src, cn, pair, c, W, aff.as<G1Aff>(), tmp.p, C.stream);
+        else
+            precompute_windows_g2((const G2Aff*)src, cn, pair, c, W, aff.as<G2Aff>(), tmp.p, C.stream);
+        SPX_HIP(hipMemcpy2DAsync(dst + j0, sizeof(A) * count, aff.p, sizeof(A) * cn, sizeof(A) * cn, W,
+                                 hipMemcpyDeviceToDevice, C.stream));
+    }
+    C.sync();
+}
+
+void pp_preprocess(Ctx& C, PP& P) {
+    const int nv = P.nv;
+    const uint64_t n = 1ull << nv;
+    P.g1_c = window_bits_for(n);
+    P.g1_W = windows_for(P.g1_c);
+    P.g1_pre.alloc(sizeof(G1Aff) * n * P.g1_W);
+    precompute_level<G1Aff>(C, P.g1_level(0), n, false, P.g1_c, P.g1_W, P.g1_pre.as<G1Aff>());
+    P.g2_off.assign(nv + 1, 0);
+    P.g2_c.assign(nv, 0);
+    P.g2_W.assign(nv, 0);
+    uint64_t tot = 0;
+    for (int i = 0; i < nv; ++i) {
+        uint64_t cnt = 1ull << (nv - i - 1);
+        P.g2_c[i] = window_bits_for(cnt);
+        P.g2_W[i] = windows_for(P.g2_c[i]);
+        P.g2_off[i] = tot;
+        tot += cnt * P.g2_W[i];
+    }
+    P.g2_off[nv] = tot;
+    P.g2_pre.alloc(sizeof(G2Aff) * std::max<uint64_t>(tot, 1));
+    for (int i = 0; i < nv; ++i) {
+        uint64_t cnt = 1ull << (nv - i - 1);
+        precompute_level<G2Aff>(C, P.g2_level(i), cnt, true, P.g2_c[i], P.g2_W[i], P.g2_pre.as<G2Aff>() + P.g2_off[i]);
+    }
+}
+
+static void pp_alloc_raw(PP& P, int nv) {
+    P.nv = nv;
+    P.lvl_off.assign(nv + 1, 0);
+    uint64_t tot = 0;
+    for (int i = 0; i < nv; ++i) {
+        P.lvl_off[i] = tot;
+        tot += 1ull << (nv - i);
+    }
+    P.lvl_off[nv] = tot;
+    P.g1_raw_mem.alloc(sizeof(G1Aff) * std::max<uint64_t>(tot, 1));
+    P.g2_raw_mem.alloc(sizeof(G2Aff) * std::max<uint64_t>(tot, 1));
+}
+
+std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len) {
+    auto P = std::make_unique<PP>();
+    size_t pos = 0;
+    auto need = [&](size_t k) {
+        if (pos + k > len) throw SpxError(kSerialization, "truncated public parameter bytes");
+    };
+    auto u64 = [&]() {
+        need(8);
+        uint64_t v;
+        memcpy(&v, b + pos, 8);
+        pos += 8;
+        return v;
+    };
+    uint64_t nv = u64();
+    if (nv < 1 || nv > 30) throw SpxError(kSerialization, "bad public parameter nv");
+    if (u64() != nv) throw SpxError(kSerialization, "powers_of_g length != nv");
+    pp_alloc_raw(*P, (int)nv);
+    std::vector<size_t> g1_pos(nv), g2_pos(nv);
+    for (uint64_t i = 0; i < nv; ++i) {
+        if (u64() != (1ull << (nv - i))) throw SpxError(kSerialization, "powers_of_g level size");
+        need(96ull << (nv - i));
+        g1_pos[i] = pos;
+        pos += 96ull << (nv - i);
+    }
+    if (u64() != nv) throw SpxError(kSerialization, "powers_of_h length != nv");
+    for (uint64_t i = 0; i < nv; ++i) {
+        if (u64() != (1ull << (nv - i))) throw SpxError(kSerialization, "powers_of_h level size");
+        need(192ull << (nv - i));
+        g2_pos[i] = pos;
+        pos += 192ull << (nv - i);
+    }
+    need(96 + 192);
+    if (!host::g1_from_uncompressed(P->g, b + pos) || !host::g2_from_uncompressed(P->h, b + pos + 96))
+        throw SpxError(kSerialization, "bad g / h");
+    for (uint64_t i = 0; i < nv; ++i) {
+        SPX_HIP(hipMemcpyAsync(P->g1_level((int)i), b + g1_pos[i], 96ull << (nv - i), hipMemcpyHostToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(P->g2_level((int)i), b + g2_pos[i], 192ull << (nv - i), hipMemcpyHostToDevice, C.stream));
+    }
+    DevMem err(sizeof(int));
+    SPX_HIP(hipMemsetAsync(err.p, 0, sizeof(int), C.stream));
+    launch_points_from_bytes_g1(P->g1_raw_mem.as<G1Aff>(), P->lvl_off[nv], err.as<int>(), C.stream);
+    launch_points_from_bytes_g2(P->g2_raw_mem.as<G2Aff>(), P->lvl_off[nv], err.as<int>(), C.stream);
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical coordinate in public parameters");
+    pp_preprocess(C, *P);
+    return P;
+}
+
+// SplitMix64 (the synthetic-input / keygen PRNG shared with oracle/c/oracle.c)
+struct SplitMix64 {
+    uint64_t s;
+    uint64_t next() {
+        s += 0x9E3779B97F4A7C15ULL;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    }
+    HFr fr() {
+        for (;;) {
+            uint64_t c[4] = {next(), next(), next(), next() & 0x7FFFFFFFFFFFFFFFULL};
+            if (!HFr::geq_p(c)) return HFr::from_canon(c);
+        }
+    }
+};
+
+template <class F>
+static std::vector<Affine<F>> fixed_base_table(const Affine<F>& base) {
+    std::vector<host::Jac<F>> jac(32 * 256);
+    host::Jac<F> outer = host::jac_from(base);
+    for (int w = 0; w < 32; ++w) {
+        host::Jac<F> acc = host::jac_inf<F>();
+        jac[w * 256] = acc;
+        for (int d = 1; d < 256; ++d) {
+            acc = host::jac_add(acc, outer);
+            jac[w * 256 + d] = acc;
+        }
+        for (int k = 0; k < 8; ++k) outer = host::jac_dbl(outer);
+    }
+    std::vector<F> zs(jac.size());
+    for (size_t i = 0; i < jac.size(); ++i) zs[i] = jac[i].z;
+    host::batch_inverse(zs);
+    std::vector<Affine<F>> out(jac.size());
+    for (size_t i = 0; i < jac.size(); ++i) {
+        if (jac[i].z.is_zero()) {
+            out[i] = {F::zero(), F::zero(), true};  // device sentinel (0,0)
+            continue;
+        }
+        F zi2 = zs[i] * zs[i];
+        out[i] = {jac[i].x * zi2, jac[i].y * zi2 * zs[i], false};
+    }
+    return out;
+}
+template <class F, class A>
+static void upload_affine(const std::vector<Affine<F>>& v, A* dst, hipStream_t s) {
+    static_assert(sizeof(A) == 2 * sizeof(F), "layout");
+    std::vector<A> tmp(v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+        memcpy((uint8_t*)&tmp[i], &v[i].x, sizeof(F));
+        memcpy((uint8_t*)&tmp[i] + sizeof(F), &v[i].y, sizeof(F));
+    }
+    SPX_HIP(hipMemcpyAsync(dst, tmp.data(), sizeof(A) * v.size(), hipMemcpyHostToDevice, s));
+    SPX_HIP(hipStreamSynchronize(s));
+}
+
+std::unique_ptr<PP> pp_generate(Ctx& C, int nv, uint64_t seed) {
+    if (nv < 1 || nv > 28) invalid("keygen: nv out of range");
+    auto P = std::make_unique<PP>();
+    SplitMix64 rng{seed};
+    HFr gs = rng.fr(), hs = rng.fr();
+    P->t.resize(nv);
+    for (int i = 0; i < nv; ++i) P->t[i] = rng.fr();
+    P->has_t = true;
+    uint64_t c[4];
+    gs.to_canon(c);
+    P->g = host::jac_to_affine(host::jac_mul(host::jac_from(host::g1_generator()), c));
+    hs.to_canon(c);
+    P->h = host::jac_to_affine(host::jac_mul(host::jac_from(host::g2_generator()), c));
+    pp_alloc_raw(*P, nv);
+    const uint64_t tot = P->lvl_off[nv];
+    // eq(t[i..], x) scalars for every level (setup.rs:37-60), Montgomery
+    DevMem tdev(32 * nv), scal(32 * tot), lo(32 << 14), hi(32 << 14);
+    SPX_HIP(hipMemcpyAsync(tdev.p, P->t.data(), 32 * nv, hipMemcpyHostToDevice, C.stream));
+    for (int i = 0; i < nv; ++i)
+        launch_eq_table(tdev.as<Fr>() + i, nv - i, 0, 1ull << (nv - i), scal.as<Fr>() + P->lvl_off[i], lo.as<Fr>(),
+                        hi.as<Fr>(), C.stream);
+    {
+        auto tg = fixed_base_table(P->g);
+        DevMem tab(sizeof(G1Aff) * tg.size()), tmp(2 * sizeof(G1Aff) * tot);
+        upload_affine(tg, tab.as<G1Aff>(), C.stream);
+        fixed_base_g1(tab.as<G1Aff>(), scal.as<Fr>(), tot, P->g1_raw_mem.as<G1Aff>(), tmp.p, C.stream);
+        C.sync();
+    }
+    {
+        auto th = fixed_base_table(P->h);
+        DevMem tab(sizeof(G2Aff) * th.size()), tmp(2 * sizeof(G2Aff) * tot);
+        upload_affine(th, tab.as<G2Aff>(), C.stream);
+        fixed_base_g2(tab.as<G2Aff>(), scal.as<Fr>(), tot, P->g2_raw_mem.as<G2Aff>(), tmp.p, C.stream);
+        C.sync();
+    }
+    pp_preprocess(C, *P);
+    return P;
+}
+
+std::vector<uint8_t> pp_serialize(Ctx& C, const PP& P) {
+    const int nv = P.nv;
+    const uint64_t tot = P.lvl_off[nv];
+    size_t need = 8 + 8 + 8 + 96 + 192;
+    for (int i = 0; i < nv; ++i) need += 16 + (96 + 192) * (1ull << (nv - i));
+    std::vector<uint8_t> out(need);
+    DevMem t1(sizeof(G1Aff) * tot), t2(sizeof(G2Aff) * tot);
+    SPX_HIP(hipMemcpyAsync(t1.p, P.g1_raw_mem.p, sizeof(G1Aff) * tot, hipMemcpyDeviceToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(t2.p, P.g2_raw_mem.p, sizeof(G2Aff) * tot, hipMemcpyDeviceToDevice, C.stream));
+    launch_points_to_canon_g1(t1.as<G1Aff>(), tot, C.stream);
+    launch_points_to_canon_g2(t2.as<G2Aff>(), tot, C.stream);
+    std::vector<uint8_t> h1(sizeof(G1Aff) * tot), h2(sizeof(G2Aff) * tot);
+    SPX_HIP(hipMemcpyAsync(h1.data(), t1.p, h1.size(), hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h2.data(), t2.p, h2.size(), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    auto fix_inf = [](uint8_t* p, size_t bytes) {  // (0,0) sentinel -> ark-serialize infinity (x=0, y=1, flag)
+        for (size_t k = 0; k < bytes; ++k)
+            if (p[k]) return;
+        HFq zero = HFq::zero(), one = HFq::one();
+        if (bytes == 96) {
+            host::fq_to_bytes(p, zero);
+            host::fq_to_bytes(p + 48, one, host::kFlagInf);
+        } else {
+            host::fq_to_bytes(p, zero);
+            host::fq_to_bytes(p + 48, zero);
+            host::fq_to_bytes(p + 96, one);
+            host::fq_to_bytes(p + 144, zero, host::kFlagInf);
+        }
+    };
+    uint8_t* p = out.data();
+    uint64_t u = (uint64_t)nv;
+    memcpy(p, &u, 8), p += 8;
+    memcpy(p, &u, 8), p += 8;
+    for (int i = 0; i < nv; ++i) {
+        uint64_t k = 1ull << (nv - i);
+        memcpy(p, &k, 8), p += 8;
+        memcpy(p, h1.data() + 96 * P.lvl_off[i], 96 * k);
+        for (uint64_t j = 0; j < k; ++j) fix_inf(p + 96 * j, 96);
+        p += 96 * k;
+    }
+    memcpy(p, &u, 8), p += 8;
+    for (int i = 0; i < nv; ++i) {
+        uint64_t k = 1ull << (nv - i);
+        memcpy(p, &k, 8), p += 8;
+        memcpy(p, h2.data() + 192 * P.lvl_off[i], 192 * k);
+        for (uint64_t j = 0; j < k; ++j) fix_inf(p + 192 * j, 192);
+        p += 192 * k;
+    }
+    host::g1_to_uncompressed(p, P.g), p += 96;
+    host::g2_to_uncompressed(p, P.h), p += 192;
+    return out;
+}
+
+// ====================================================================== index
+static void check_csr(const HostCsr& m, uint64_t n) {
+    if (m.n != n) invalid("matrix size is inconsistent with number of constraints");
+    if (m.rp.size() != n + 1 || m.rp[0] != 0) invalid("malformed row_ptr");
+    for (uint64_t x = 0; x < n; ++x)
+        if (m.rp[x + 1] < m.rp[x]) invalid("malformed row_ptr");
+    const uint64_t nnz = m.rp[n];
+    if (m.col.size() < nnz || m.val.size() < 32 * nnz) invalid("malformed CSR arrays");
+    for (uint64_t k = 0; k < nnz; ++k)
+        if (m.col[k] >= n) invalid("sparse index out of bound");
+}
+
+// upload a rank-local block [lo, lo + cnt) of `ptr`-indexed segments, with long-row chunking
+static void upload_sparse(Ctx& C, DevSparse& D, const std::vector<uint64_t>* ptrs, const std::vector<uint32_t>* idxs,
+                          const std::vector<uint8_t>* vals, uint64_t lo, uint64_t cnt, int* err_dev) {
+    std::vector<LongChunk> chunks;
+    std::vector<LongRow> lrows;
+    for (int m = 0; m < 3; ++m) {
+        const uint64_t base = ptrs[m][lo], end = ptrs[m][lo + cnt], nnz = end - base;
+        std::vector<uint64_t> p(cnt + 1);
+        for (uint64_t x = 0; x <= cnt; ++x) p[x] = ptrs[m][lo + x] - base;
+        D.ptr[m].alloc(8 * (cnt + 1));
+        D.idx[m].alloc(4 * std::max<uint64_t>(nnz, 1));
+        D.val[m].alloc(32 * std::max<uint64_t>(nnz, 1));
+        SPX_HIP(hipMemcpyAsync(D.ptr[m].p, p.data(), 8 * (cnt + 1), hipMemcpyHostToDevice, C.stream));
+        if (nnz) {
+            SPX_HIP(hipMemcpyAsync(D.idx[m].p, idxs[m].data() + base, 4 * nnz, hipMemcpyHostToDevice, C.stream));
+            SPX_HIP(hipMemcpyAsync(D.val[m].p, vals[m].data() + 32 * base, 32 * nnz, hipMemcpyHostToDevice, C.stream));
+            launch_to_mont(D.val[m].as<Fr>(), nnz, err_dev, C.stream);
+        }
+        for (uint64_t x = 0; x < cnt; ++x) {
+            if (p[x + 1] - p[x] <= kLongRow) continue;
+            LongRow lr{};
+            lr.m = (uint32_t)m;
+            lr.x = x;
+            lr.chunk_begin = (uint32_t)chunks.size();
+            for (uint64_t k = p[x]; k < p[x + 1]; k += kChunk) {
+                LongChunk ch{};
+                ch.m = (uint32_t)m;
+                ch.begin = k;
+                ch.end = std::min(k + kChunk, p[x + 1]);
+                chunks.push_back(ch);
+            }
+            lr.chunk_end = (uint32_t)chunks.size();
+            lrows.push_back(lr);
+        }
+        C.sync();  // host vectors go out of scope
+    }
+    D.nchunks = (int)chunks.size();
+    D.nlrows = (int)lrows.size();
+    if (D.nchunks) {
+        D.chunks.alloc(sizeof(LongChunk) * chunks.size());
+        D.lrows.alloc(sizeof(LongRow) * lrows.size());
+        SPX_HIP(hipMemcpyAsync(D.chunks.p, chunks.data(), sizeof(LongChunk) * chunks.size(), hipMemcpyHostToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(D.lrows.p, lrows.data(), sizeof(LongRow) * lrows.size(), hipMemcpyHostToDevice, C.stream));
+        C.sync();
+    }
+}
+
+static void feed_matrix(Blake2s& h, const HostCsr& m) {
+    // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize }
+    std::vector<uint8_t> buf;
+    buf.reserve(1 << 16);
+    auto flush = [&]() {
+        h.update(buf.data(), buf.size());
+        buf.clear();
+    };
+    auto put64 = [&](uint64_t v) {
+        uint8_t b[8];
+        memcpy(b, &v, 8);
+        buf.insert(buf.end(), b, b + 8);
+    };
+    put64(m.n);
+    for (uint64_t x = 0; x < m.n; ++x) {
+        put64(m.rp[x + 1] - m.rp[x]);
+        for (uint64_t k = m.rp[x]; k < m.rp[x + 1]; ++k) {
+            buf.insert(buf.end(), m.val.data() + 32 * k, m.val.data() + 32 * k + 32);
+            put64(m.col[k]);
+        }
+        if (buf.size() > (1 << 16) - 4096) flush();
+    }
+    put64(m.n);
+    flush();
+}
+
+std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
+    auto I = std::make_unique<Index>();
+    const uint64_t n = mats[0].n;
+    if (!is_pow2(n)) invalid("Matrix width should be a power of 2.");  // indexer.rs:49-51
+    if (n < 2) invalid("at least 2 constraints are required");
+    for (int m = 0; m < 3; ++m) check_csr(mats[m], n);
+    I->n = n;
+    I->log_n = ilog2(n);
+    for (int m = 0; m < 3; ++m) I->m[m] = mats[m];
+    const int G = C.comm->size(), rank = C.comm->rank();
+    if (!is_pow2((uint64_t)G) || (uint64_t)G > n / 2) invalid("world size must be a power of two <= n / 2");
+    I->G = G;
+    I->rank = rank;
+    const uint64_t nl = n / G, lo = (uint64_t)rank * nl;
+    DevMem err(sizeof(int));
+    SPX_HIP(hipMemsetAsync(err.p, 0, sizeof(int), C.stream));
+    // rows (CSR) for sum_over_y
+    std::vector<uint64_t> rps[3];
+    std::vector<uint32_t> cols[3];
+    std::vector<uint8_t> vals[3];
+    for (int m = 0; m < 3; ++m) rps[m] = mats[m].rp;
+    {
+        const std::vector<uint32_t>* ci[3] = {&mats[0].col, &mats[1].col, &mats[2].col};
+        const std::vector<uint8_t>* vi[3] = {&mats[0].val, &mats[1].val, &mats[2].val};
+        std::vector<uint32_t> c3[3];
+        std::vector<uint8_t> v3[3];
+        for (int m = 0; m < 3; ++m) c3[m] = *ci[m], v3[m] = *vi[m];
+        upload_sparse(C, I->rows, rps, c3, v3, lo, nl, err.as<int>());
+    }
+    // columns (CSC, stable counting sort: rows ascending within a column) for eval_on_x
+    for (int m = 0; m < 3; ++m) {
+        const HostCsr& M = mats[m];
+        const uint64_t nnz = M.rp[n];
+        std::vector<uint64_t> cp(n + 1, 0);
+        for (uint64_t k = 0; k < nnz; ++k) cp[M.col[k] + 1]++;
+        for (uint64_t y = 0; y < n; ++y) cp[y + 1] += cp[y];
+        std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
+        cols[m].assign(nnz, 0);
+        vals[m].assign(32 * nnz, 0);
+        for (uint64_t x = 0; x < n; ++x)
+            for (uint64_t k = M.rp[x]; k < M.rp[x + 1]; ++k) {
+                uint64_t pos = cur[M.col[k]]++;
+                cols[m][pos] = (uint32_t)x;
+                memcpy(&vals[m][32 * pos], &M.val[32 * k], 32);
+            }
+        rps[m] = std::move(cp);
+    }
+    upload_sparse(C, I->cols, rps, cols, vals, lo, nl, err.as<int>());
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical field element in matrix");
+    // witness-independent transcript prefix (lib.rs:61-64), absorbed once
+    for (int m = 0; m < 3; ++m) feed_matrix(I->cache, mats[m]);
+    I->has_cache = true;
+    return I;
+}
+
+std::unique_ptr<Witness> witness_upload(Ctx& C, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw) {
+    if (!is_pow2(nv)) invalid("public input should be power of two");  // prover.rs:114-116
+    auto W = std::make_unique<Witness>();
+    W->n = nv + nw;
+    W->v.assign(v, v + 32 * nv);
+    W->z.alloc(32 * std::max<uint64_t>(W->n, 1));
+    SPX_HIP(hipMemcpyAsync(W->z.p, v, 32 * nv, hipMemcpyHostToDevice, C.stream));
+    if (nw) SPX_HIP(hipMemcpyAsync(W->z.as<uint8_t>() + 32 * nv, w, 32 * nw, hipMemcpyHostToDevice, C.stream));
+    DevMem err(sizeof(int));
+    SPX_HIP(hipMemsetAsync(err.p, 0, sizeof(int), C.stream));
+    launch_to_mont(W->z.as<Fr>(), W->n, err.as<int>(), C.stream);
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical field element in witness");
+    return W;
+}
+
+// ====================================================================== prove helpers
+struct Ser {
+    std::vector<uint8_t> b;
+    void u64(uint64_t v) {
+        uint8_t t[8];
+        memcpy(t, &v, 8);
+        b.insert(b.end(), t, t + 8);
+    }
+    void fr(const HFr& x) {
+        uint8_t t[32];
+        host::fr_to_bytes(t, x);
+        b.insert(b.end(), t, t + 32);
+    }
+    void raw(const uint8_t* p, size_t k) { b.insert(b.end(), p, p + k); }
+};
+
+static HFr ld_hfr(const uint8_t* p) {  // device Montgomery bytes -> host Fr
+    HFr r;
+    memcpy(r.v, p, 32);
+    return r;
+}
+static HFr eq1(const HFr& tau, const HFr& t) {  // eq(tau, t) = 1 - tau - t + 2 tau t  (eq.rs:14)
+    HFr tt = tau * t;
+    return HFr::one() - tau - t + tt + tt;
+}
+
+size_t proof_size(int L) {
+    const size_t open = 32 + 96 + 8 + 96 * (size_t)L;
+    return 56 + open + 16 + 8 + (size_t)L * (8 + 32 * (size_t)(L + 3)) + 96 + 16 + 8 + (size_t)L * (8 + 96) + open;
+}
+
+struct Timer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double us() const {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
+template <class F>
+static Affine<F> xyzz_bytes_to_affine(const uint8_t* p) {
+    F X, Y, ZZ, ZZZ;
+    memcpy(&X, p, sizeof(F));
+    memcpy(&Y, p + sizeof(F), sizeof(F));
+    memcpy(&ZZ, p + 2 * sizeof(F), sizeof(F));
+    memcpy(&ZZZ, p + 3 * sizeof(F), sizeof(F));
+    return host::xyzz_to_affine(X, Y, ZZ, ZZZ);
+}
+
+// sum of affine points gathered from every rank
+template <class F>
+static Affine<F> sum_affine(const std::vector<Affine<F>>& pts) {
+    host::Jac<F> acc = host::jac_inf<F>();
+    for (auto& p : pts) acc = host::jac_add(acc, host::jac_from(p));
+    return host::jac_to_affine(acc);
+}
+
+template <class F>
+static std::vector<Affine<F>> allgather_affine(Comm& comm, const Affine<F>& mine) {
+    const int G = comm.size();
+    std::vector<Affine<F>> all(G);
+    comm.allgather(&mine, all.data(), sizeof(Affine<F>));
+    return all;
+}
+
+static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
+    const int G = comm.size();
+    std::vector<HFr> all(mine.size() * G);
+    comm.allgather(mine.data(), all.data(), sizeof(HFr) * mine.size());
+    return all;
+}
+
+// ---------------------------------------------------------------- commit (commit.rs:17-29)
+static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
+    const uint64_t nl = n / G, lo = (uint64_t)rank * nl;
+    MsmInst inst{};
+    inst.pts_off = lo;
+    inst.stride = (uint32_t)n;
+    inst.scalar_off = lo;
+    inst.size = (uint32_t)nl;
+    inst.c = (uint32_t)P.g1_c;
+    inst.W = (uint32_t)P.g1_W;
+    DevMem out(4 * sizeof(Fq));
+    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out.p, C.stream);
+    uint8_t* h = C.pinned(4 * sizeof(Fq));
+    SPX_HIP(hipMemcpyAsync(h, out.p, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(h);
+    if (G == 1) return part;
+    return sum_affine(allgather_affine(*C.comm, part));
+}
+
+// ---------------------------------------------------------------- open (open.rs:19-58)
+struct OpenOut {
+    HFr eval;
+    std::vector<Affine<HFq2>> proofs;
+};
+static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector<HFr>& point, int G, int rank) {
+    const int g = ilog2((uint64_t)G);
+    const uint64_t nl = (1ull << L) / G;
+    const int nloc = L - g;  // local levels
+    OpenOut res;
+    res.proofs.resize(L);
+    DevMem pt(32 * L), q(32 * std::max<uint64_t>(nl, 1)), ra(32 * std::max<uint64_t>(nl / 2, 1)),
+        rb(32 * std::max<uint64_t>(nl / 4, 1));
+    SPX_HIP(hipMemcpyAsync(pt.p, point.data(), 32 * L, hipMemcpyHostToDevice, C.stream));
+    std::vector<MsmInst> insts(nloc);
+    const Fr* rin = z_local;
+    Fr* bufs[2] = {ra.as<Fr>(), rb.as<Fr>()};
+    uint64_t qoff = 0;
+    for (int i = 0; i < nloc; ++i) {
+        const uint64_t half = nl >> (i + 1);
+        Fr* rout = bufs[i & 1];
+        launch_open_level(rin, rout, q.as<Fr>() + qoff, pt.as<Fr>() + i, half, C.stream);
+        MsmInst& I = insts[i];
+        const uint64_t full = 1ull << (L - i - 1);
+        I.pts_off = P.g2_off[i] + (uint64_t)rank * half;
+        I.stride = (uint32_t)full;
+        I.scalar_off = qoff;
+        I.size = (uint32_t)half;
+        I.c = (uint32_t)P.g2_c[i];
+        I.W = (uint32_t)P.g2_W[i];
+        qoff += half;
+        rin = rout;
+    }
+    DevMem out(4 * sizeof(Fq2) * std::max(nloc, 1));
+    msm_run_g2(C.msm, insts.data(), nloc, P.g2_pre.as<G2Aff>(), q.as<Fr>(), out.p, C.stream);
+    const size_t xb = 4 * sizeof(Fq2);
+    uint8_t* h = C.pinned(xb * nloc + 32);
+    SPX_HIP(hipMemcpyAsync(h, out.p, xb * nloc, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h + xb * nloc, rin, 32, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    std::vector<Affine<HFq2>> part(nloc);
+    for (int i = 0; i < nloc; ++i) part[i] = xyzz_bytes_to_affine<HFq2>(h + xb * i);
+    HFr rlast = ld_hfr(h + xb * nloc);
+    if (G == 1) {
+        res.proofs = part;
+        res.eval = rlast;
+        return res;
+    }
+    // gather partial proofs and the one remaining local value per rank
+    {
+        std::vector<Affine<HFq2>> all(nloc * G);
+        C.comm->allgather(part.data(), all.data(), sizeof(Affine<HFq2>) * nloc);
+        for (int i = 0; i < nloc; ++i) {
+            std::vector<Affine<HFq2>> v(G);
+            for (int r = 0; r < G; ++r) v[r] = all[r * nloc + i];
+            res.proofs[i] = sum_affine(v);
+        }
+    }
+    std::vector<HFr> rg = allgather_fr(*C.comm, {rlast});  // global r_g table (G entries)
+    // remaining g levels on the gathered table; tiny MSMs run redundantly on every rank
+    std::vector<HFr> qs;
+    std::vector<MsmInst> tinsts;
+    for (int i = nloc; i < L; ++i) {
+        const uint64_t half = rg.size() / 2;
+        std::vector<HFr> nr(half);
+        MsmInst I{};
+        I.pts_off = P.g2_off[i];
+        I.stride = (uint32_t)half;
+        I.scalar_off = qs.size();
+        I.size = (uint32_t)half;
+        I.c = (uint32_t)P.g2_c[i];
+        I.W = (uint32_t)P.g2_W[i];
+        for (uint64_t b = 0; b < half; ++b) {
+            HFr qq = rg[2 * b + 1] - rg[2 * b];
+            qs.push_back(qq);
+            nr[b] = rg[2 * b] + point[i] * qq;
+        }
+        rg.swap(nr);
+        tinsts.push_back(I);
+    }
+    res.eval = rg[0];
+    DevMem qd(32 * qs.size()), out2(xb * tinsts.size());
+    SPX_HIP(hipMemcpyAsync(qd.p, qs.data(), 32 * qs.size(), hipMemcpyHostToDevice, C.stream));
+    msm_run_g2(C.msm, tinsts.data(), (int)tinsts.size(), P.g2_pre.as<G2Aff>(), qd.as<Fr>(), out2.p, C.stream);
+    uint8_t* h2 = C.pinned(xb * tinsts.size());
+    SPX_HIP(hipMemcpyAsync(h2, out2.p, xb * tinsts.size(), hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    for (size_t k = 0; k < tinsts.size(); ++k) res.proofs[nloc + k] = xyzz_bytes_to_affine<HFq2>(h2 + xb * k);
+    return res;
+}
+
+static void ser_open(Ser& s, const HFr& eval, const PP& P, const std::vector<Affine<HFq2>>& proofs) {
+    s.fr(eval);
+    uint8_t b[96];
+    host::g2_compress(b, P.h);
+    s.raw(b, 96);
+    s.u64(proofs.size());
+    for (auto& p : proofs) {
+        host::g2_compress(b, p);
+        s.raw(b, 96);
+    }
+}
+
+// sumcheck #1 message from G(0), G(1), G(2): P(t) = C eq(tau_c, t) G(t), t = 0..L+2
+static std::vector<HFr> sc1_message(const HFr& Cc, const HFr& tau, const HFr g[3], int L) {
+    static const HFr inv2 = HFr::from_u64(2).inv();
+    std::vector<HFr> P(L + 3);
+    const HFr one = HFr::one(), two = HFr::from_u64(2);
+    for (int t = 0; t <= L + 2; ++t) {
+        HFr T = HFr::from_u64((uint64_t)t);
+        HFr l0 = (T - one) * (T - two) * inv2, l1 = T * (T - two), l2 = T * (T - one) * inv2;
+        HFr Gt = g[0] * l0 - g[1] * l1 + g[2] * l2;
+        P[t] = Cc * eq1(tau, T) * Gt;
+    }
+    return P;
+}
+
+// ====================================================================== prove
+std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts& o) {
+    Timer tall;
+    C.timings.clear();
+    auto mark = [&](const char* name, Timer& t) {
+        C.timings.emplace_back(name, t.us());
+        t = Timer();
+    };
+    Timer tp;
+    const int L = I.log_n;
+    const uint64_t n = I.n;
+    Comm& comm = *C.comm;
+    const int G = comm.size(), rank = comm.rank();
+    if (G != I.G || rank != I.rank) invalid("index was built for a different communicator");
+    const int g = ilog2((uint64_t)G);
+    const uint64_t nl = n / G, lo = (uint64_t)rank * nl;
+    const uint64_t nvv = W.v.size() / 32;
+    if (!is_pow2(nvv)) invalid("public input should be power of two");
+    if (W.n != n) invalid("|v| + |w| != number of variables");  // prover.rs:117-119
+    if (P.nv != L) invalid("public parameter nv != log_n");
+    const int log_v = ilog2(nvv);
+    Transcript T(o.mode == 1, o.seed);
+    if (o.cached && I.has_cache)
+        T.set_state(I.cache);
+    else {
+        Blake2s h;
+        for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        T.set_state(h);
+    }
+    {
+        Ser s;
+        s.u64(nvv);
+        s.raw(W.v.data(), W.v.size());
+        T.feed(s.b.data(), s.b.size());
+    }
+    mark("transcript_matrices", tp);
+    const Fr* z = W.z.as<Fr>();
+    const Fr* zl = z + lo;
+    // scratch layout (Fr units)
+    const uint64_t n2 = std::max<uint64_t>(nl / 2, 1), n4 = std::max<uint64_t>(nl / 4, 1);
+    const uint64_t need = 3 * nl        // Az Bz Cz
+                          + 3 * n2 + 3 * n4  // fold ping-pong
+                          + n2 + n4 + std::max<uint64_t>(nl / 8, 1)  // E tables
+                          + n                // eq(r_x)
+                          + nl + n2 + n4     // Mrx + fold
+                          + n2 + n4          // z fold
+                          + std::max<uint64_t>(3 * 2048, std::max(I.rows.nchunks, I.cols.nchunks))
+                          + 8192 * 2 + 64 + 8 * L;  // partials, eq scratch, challenges
+    C.scratch.ensure(32 * need);
+    Fr* base = C.scratch.as<Fr>();
+    uint64_t cur_off = 0;
+    auto take = [&](uint64_t k) {
+        Fr* p = base + cur_off;
+        cur_off += k;
+        return p;
+    };
+    Fr *Az = take(nl), *Bz = take(nl), *Cz = take(nl);
+    Fr* F1[3] = {take(n2), take(n2), take(n2)};
+    Fr* F2[3] = {take(n4), take(n4), take(n4)};
+    Fr *E1 = take(n2), *Ea = take(n4), *Eb = take(std::max<uint64_t>(nl / 8, 1));
+    Fr* EQ = take(n);
+    Fr *M0 = take(nl), *M1 = take(n2), *M2 = take(n4);
+    Fr *Z1 = take(n2), *Z2 = take(n4);
+    Fr* partial = take(std::max<uint64_t>(3 * 2048, std::max(I.rows.nchunks, I.cols.nchunks)));
+    Fr *eqlo = take(8192), *eqhi = take(8192);
+    Fr* res3 = take(64);
+    Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
+    uint8_t* hp = C.pinned(1 << 16);
+
+    // ---- SpMV Az, Bz, Cz (challenge-independent: queued first, overlaps the commit's host work)
+    {
+        SparseView3 rv = I.rows.view();
+        launch_sparse3(0, rv, z, Az, Bz, Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(), I.rows.nchunks,
+                       I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
+    }
+    // ---- round 1: commitment (prover.rs:123-141)
+    Affine<HFq> com = commit_z(C, P, z, n, G, rank);
+    Ser proof;
+    {
+        size_t m0 = proof.b.size();
+        proof.u64((uint64_t)L);
+        uint8_t b[48];
+        host::g1_compress(b, com);
+        proof.raw(b, 48);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+    }
+    mark("commit", tp);
+    // ---- round 2: open at (r_v, 0...0) (prover.rs:143-160)
+    std::vector<HFr> pt1(L, HFr::zero());
+    for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
+    {
+        OpenOut op = open_z(C, P, zl, L, pt1, G, rank);
+        size_t m0 = proof.b.size();
+        ser_open(proof, op.eval, P, op.proofs);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+    }
+    mark("open_rv", tp);
+    // ---- round 3: tau, eq, sumcheck #1 setup (prover.rs:163-196)
+    std::vector<HFr> tau(L);
+    for (int i = 0; i < L; ++i) tau[i] = T.rand_fr();
+    memcpy(hp, tau.data(), 32 * L);
+    SPX_HIP(hipMemcpyAsync(chdev, hp, 32 * L, hipMemcpyHostToDevice, C.stream));
+    // E_1[b] = eq(tau_1..tau_{L-1}, b) on this rank's block of b
+    if (L >= 2)
+        launch_eq_table(chdev + 1, L - 1, (uint64_t)rank * (nl / 2), nl / 2, E1, eqlo, eqhi, C.stream);
+    else {
+        HFr one = HFr::one();
+        SPX_HIP(hipMemcpyAsync(E1, &one, 32, hipMemcpyHostToDevice, C.stream));
+    }
+    {
+        size_t m0 = proof.b.size();
+        proof.u64((uint64_t)(L + 2));  // IndexInfo.max_multiplicands (reconstructed field order)
+        proof.u64((uint64_t)L);        // IndexInfo.num_variables
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+    }
+    // ---- sumcheck #1 (lib.rs:86-103)
+    proof.u64((uint64_t)L);
+    std::vector<HFr> r_x;
+    HFr Cc = HFr::one();
+    Fr* rdev = chdev + L;  // challenges r_1.. on device
+    Tables3 cur{{Az, Bz, Cz}};
+    const Fr* Ecur = E1;
+    Fr* Ebuf[2] = {Ea, Eb};
+    for (int i = 1; i <= L - g; ++i) {
+        const uint64_t half = nl >> i;
+        const bool fold = i >= 2;
+        Tables3 out{{nullptr, nullptr, nullptr}};
+        Fr* Eout = nullptr;
+        if (fold) {
+            Fr** fb = (i % 2 == 0) ? F1 : F2;
+            out = Tables3{{fb[0], fb[1], fb[2]}};
+            if (i < L - g) Eout = Ebuf[i & 1];
+        }
+        launch_sc1_round(fold, cur, out, Ecur, Eout, fold ? rdev + (i - 2) : nullptr, half, partial, res3, C.stream);
+        SPX_HIP(hipMemcpyAsync(hp, res3, 96, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+        HFr gs[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
+        if (G > 1) {
+            std::vector<HFr> all = allgather_fr(comm, {gs[0], gs[1], gs[2]});
+            gs[0] = gs[1] = gs[2] = HFr::zero();
+            for (int r = 0; r < G; ++r)
+                for (int k = 0; k < 3; ++k) gs[k] += all[3 * r + k];
+        }
+        std::vector<HFr> msg = sc1_message(Cc, tau[i - 1], gs, L);
+        size_t m0 = proof.b.size();
+        proof.u64(msg.size());
+        for (auto& e : msg) proof.fr(e);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+        HFr ch = T.rand_fr();
+        r_x.push_back(ch);
+        Cc = Cc * eq1(tau[i - 1], ch);
+        memcpy(hp + 128, &ch, 32);
+        SPX_HIP(hipMemcpyAsync(rdev + (i - 1), hp + 128, 32, hipMemcpyHostToDevice, C.stream));
+        if (fold) {
+            cur = out;
+            if (Eout) Ecur = Eout;
+        }
+    }
+    // local tables now hold 2 entries each (folded up to r_{L-g-1}); bind r_{L-g} on the host
+    HFr va, vb, vc;
+    {
+        for (int m = 0; m < 3; ++m) SPX_HIP(hipMemcpyAsync(hp + 64 * m, cur.t[m], 64, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+        const HFr r = r_x.back();
+        std::vector<HFr> mine(3);
+        for (int m = 0; m < 3; ++m) {
+            HFr a0 = ld_hfr(hp + 64 * m), a1 = ld_hfr(hp + 64 * m + 32);
+            mine[m] = a0 + r * (a1 - a0);
+        }
+        std::vector<HFr> tabs[3];
+        if (G == 1) {
+            for (int m = 0; m < 3; ++m) tabs[m] = {mine[m]};
+        } else {
+            std::vector<HFr> all = allgather_fr(comm, mine);
+            for (int m = 0; m < 3; ++m)
+                for (int r2 = 0; r2 < G; ++r2) tabs[m].push_back(all[3 * r2 + m]);
+        }
+        // last g rounds on the gathered tables (size 2^g), same message formula
+        for (int i = L - g + 1; i <= L; ++i) {
+            const size_t half = tabs[0].size() / 2;
+            const int c = i - 1;
+            HFr gs[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
+            for (size_t b = 0; b < half; ++b) {
+                HFr e = HFr::one();  // eq(tau_{c+1..L-1}, b)
+                for (int j = c + 1; j < L; ++j) e *= ((b >> (j - c - 1)) & 1) ? tau[j] : HFr::one() - tau[j];
+                HFr x0[3], x1[3], y[3];
+                for (int m = 0; m < 3; ++m) {
+                    x0[m] = tabs[m][2 * b];
+                    x1[m] = tabs[m][2 * b + 1];
+                    y[m] = x1[m] + x1[m] - x0[m];
+                }
+                gs[0] += (x0[0] * x0[1] - x0[2]) * e;
+                gs[1] += (x1[0] * x1[1] - x1[2]) * e;
+                gs[2] += (y[0] * y[1] - y[2]) * e;
+            }
+            std::vector<HFr> msg = sc1_message(Cc, tau[c], gs, L);
+            size_t m0 = proof.b.size();
+            proof.u64(msg.size());
+            for (auto& e : msg) proof.fr(e);
+            T.feed(proof.b.data() + m0, proof.b.size() - m0);
+            HFr ch = T.rand_fr();
+            r_x.push_back(ch);
+            Cc = Cc * eq1(tau[c], ch);
+            for (int m = 0; m < 3; ++m) {
+                std::vector<HFr> nt(half);
+                for (size_t b = 0; b < half; ++b) nt[b] = tabs[m][2 * b] + ch * (tabs[m][2 * b + 1] - tabs[m][2 * b]);
+                tabs[m].swap(nt);
+            }
+        }
+        va = tabs[0][0];
+        vb = tabs[1][0];
+        vc = tabs[2][0];
+    }
+    mark("sumcheck1", tp);
+    // ---- round 4 (prover.rs:210-228)
+    {
+        size_t m0 = proof.b.size();
+        proof.fr(va);
+        proof.fr(vb);
+        proof.fr(vc);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+    }
+    HFr rabc[3] = {T.rand_fr(), T.rand_fr(), T.rand_fr()};
+    // ---- round 5: M_rx = sum_m r_m M(r_x, .) on this rank's columns (prover.rs:230-255)
+    Fr* rxdev = chdev + 2 * L;  // r_x (L) then r_abc (3)
+    memcpy(hp, r_x.data(), 32 * L);
+    memcpy(hp + 32 * L, rabc, 96);
+    SPX_HIP(hipMemcpyAsync(rxdev, hp, 32 * (L + 3), hipMemcpyHostToDevice, C.stream));
+    launch_eq_table(rxdev, L, 0, n, EQ, eqlo, eqhi, C.stream);
+    {
+        SparseView3 cv = I.cols.view();
+        launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, rxdev + L, nl, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
+                       I.cols.lrows.as<LongRow>(), I.cols.nlrows, partial, C.stream);
+    }
+    {
+        size_t m0 = proof.b.size();
+        proof.u64(2);
+        proof.u64((uint64_t)L);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+    }
+    mark("eval_on_x", tp);
+    // ---- sumcheck #2 (lib.rs:114-131)
+    proof.u64((uint64_t)L);
+    std::vector<HFr> r_y;
+    Fr* r2dev = chdev + 3 * L + 3;
+    const Fr* Mc = M0;
+    const Fr* Zc = zl;
+    Fr* Mb[2] = {M1, M2};
+    Fr* Zb[2] = {Z1, Z2};
+    for (int i = 1; i <= L - g; ++i) {
+        const uint64_t half = nl >> i;
+        const bool fold = i >= 2;
+        Fr* Mo = fold ? Mb[i & 1] : nullptr;
+        Fr* Zo = fold ? Zb[i & 1] : nullptr;
+        launch_sc2_round(fold, Mc, Zc, Mo, Zo, fold ? r2dev + (i - 2) : nullptr, half, partial, res3, C.stream);
+        SPX_HIP(hipMemcpyAsync(hp, res3, 96, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+        HFr ps[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
+        if (G > 1) {
+            std::vector<HFr> all = allgather_fr(comm, {ps[0], ps[1], ps[2]});
+            ps[0] = ps[1] = ps[2] = HFr::zero();
+            for (int r = 0; r < G; ++r)
+                for (int k = 0; k < 3; ++k) ps[k] += all[3 * r + k];
+        }
+        size_t m0 = proof.b.size();
+        proof.u64(3);
+        for (int k = 0; k < 3; ++k) proof.fr(ps[k]);
+        T.feed(proof.b.data() + m0, proof.b.size() - m0);
+        HFr ch = T.rand_fr();
+        r_y.push_back(ch);
+        memcpy(hp + 128, &ch, 32);
+        SPX_HIP(hipMemcpyAsync(r2dev + (i - 1), hp + 128, 32, hipMemcpyHostToDevice, C.stream));
+        if (fold) {
+            Mc = Mo;
+            Zc = Zo;
+        }
+    }
+    if (g > 0) {
+        SPX_HIP(hipMemcpyAsync(hp, Mc, 64, hipMemcpyDeviceToHost, C.stream));
+        SPX_HIP(hipMemcpyAsync(hp + 64, Zc, 64, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+        const HFr r = r_y.back();
+        std::vector<HFr> mine(2);
+        for (int k = 0; k < 2; ++k) {
+            HFr a0 = ld_hfr(hp + 64 * k), a1 = ld_hfr(hp + 64 * k + 32);
+            mine[k] = a0 + r * (a1 - a0);
+        }
+        std::vector<HFr> all = allgather_fr(comm, mine), Mt, Zt;
+        for (int r2 = 0; r2 < G; ++r2) Mt.push_back(all[2 * r2]), Zt.push_back(all[2 * r2 + 1]);
+        for (int i = L - g + 1; i <= L; ++i) {
+            const size_t half = Mt.size() / 2;
+            HFr ps[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
+            for (size_t b = 0; b < half; ++b) {
+                HFr m0v = Mt[2 * b], m1v = Mt[2 * b + 1], z0 = Zt[2 * b], z1 = Zt[2 * b + 1];
+                ps[0] += m0v * z0;
+                ps[1] += m1v * z1;
+                ps[2] += (m1v + m1v - m0v) * (z1 + z1 - z0);
+            }
+            size_t m0 = proof.b.size();
+            proof.u64(3);
+            for (int k = 0; k < 3; ++k) proof.fr(ps[k]);
+            T.feed(proof.b.data() + m0, proof.b.size() - m0);
+            HFr ch = T.rand_fr();
+            r_y.push_back(ch);
+            std::vector<HFr> nm(half), nz(half);
+            for (size_t b = 0; b < half; ++b) {
+                nm[b] = Mt[2 * b] + ch * (Mt[2 * b + 1] - Mt[2 * b]);
+                nz[b] = Zt[2 * b] + ch * (Zt[2 * b + 1] - Zt[2 * b]);
+            }
+            Mt.swap(nm);
+            Zt.swap(nz);
+        }
+    }
+    mark("sumcheck2", tp);
+    // ---- round 6: open at r_y (prover.rs:268-281)
+    {
+        OpenOut op = open_z(C, P, zl, L, r_y, G, rank);
+        ser_open(proof, op.eval, P, op.proofs);
+    }
+    mark("open_ry", tp);
+    C.timings.emplace_back("total", tall.us());
+    return proof.b;
+}
+
+// ====================================================================== kernel-level entry points
+static HostCsr single(const HostCsr& m) { return m; }
+
+std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z) {
+    const uint64_t n = m.n;
+    check_csr(m, n);
+    HostCsr empty;
+    empty.n = n;
+    empty.rp.assign(n + 1, 0);
+    HostCsr mats[3] = {single(m), empty, empty};
+    DevSparse D;
+    std::vector<uint64_t> rps[3] = {mats[0].rp, mats[1].rp, mats[2].rp};
+    std::vector<uint32_t> cols[3] = {mats[0].col, mats[1].col, mats[2].col};
+    std::vector<uint8_t> vals[3] = {mats[0].val, mats[1].val, mats[2].val};
+    DevMem err(sizeof(int)), zd(32 * n), out(32 * n * 3), part(32 * 4096);
+    SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
+    upload_sparse(C, D, rps, cols, vals, 0, n, err.as<int>());
+    SPX_HIP(hipMemcpyAsync(zd.p, z, 32 * n, hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(zd.as<Fr>(), n, err.as<int>(), C.stream);
+    Fr* o = out.as<Fr>();
+    if (D.nchunks > (int)4096) part.alloc(32 * D.nchunks);
+    launch_sparse3(0, D.view(), zd.as<Fr>(), o, o + n, o + 2 * n, nullptr, n, D.chunks.as<LongChunk>(), D.nchunks,
+                   D.lrows.as<LongRow>(), D.nlrows, part.as<Fr>(), C.stream);
+    launch_from_mont(o + n, o, n, C.stream);
+    std::vector<uint8_t> res(32 * n);
+    SPX_HIP(hipMemcpyAsync(res.data(), o + n, 32 * n, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    return res;
+}
+
+std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
+    const uint64_t n = m.n;
+    check_csr(m, n);
+    if (!is_pow2(n)) invalid("2^(r_x) should have size: num_constraints");
+    const int L = ilog2(n);
+    // CSC of m (matrices B, C empty), scale (1, 0, 0)
+    const uint64_t nnz = m.rp[n];
+    std::vector<uint64_t> cp(n + 1, 0);
+    for (uint64_t k = 0; k < nnz; ++k) cp[m.col[k] + 1]++;
+    for (uint64_t y = 0; y < n; ++y) cp[y + 1] += cp[y];
+    std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
+    std::vector<uint32_t> rows(nnz);
+    std::vector<uint8_t> vals(32 * nnz);
+    for (uint64_t x = 0; x < n; ++x)
+        for (uint64_t k = m.rp[x]; k < m.rp[x + 1]; ++k) {
+            uint64_t pos = cur[m.col[k]]++;
+            rows[pos] = (uint32_t)x;
+            memcpy(&vals[32 * pos], &m.val[32 * k], 32);
+        }
+    std::vector<uint64_t> rps[3] = {cp, std::vector<uint64_t>(n + 1, 0), std::vector<uint64_t>(n + 1, 0)};
+    std::vector<uint32_t> cols[3] = {rows, {}, {}};
+    std::vector<uint8_t> vv[3] = {vals, {}, {}};
+    DevSparse D;
+    DevMem err(sizeof(int)), rx(32 * L + 96), eq(32 * n), out(32 * n * 2), part(32 * std::max(4096, 1)), lo(32 << 14),
+        hi(32 << 14);
+    SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
+    upload_sparse(C, D, rps, cols, vv, 0, n, err.as<int>());
+    std::vector<uint8_t> hr(32 * L + 96, 0);
+    memcpy(hr.data(), r_x, 32 * L);
+    HFr one = HFr::one();
+    uint64_t onec[4];
+    one.to_canon(onec);
+    memcpy(hr.data() + 32 * L, onec, 32);  // canonical 1, 0, 0
+    SPX_HIP(hipMemcpyAsync(rx.p, hr.data(), hr.size(), hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(rx.as<Fr>(), L + 3, err.as<int>(), C.stream);
+    launch_eq_table(rx.as<Fr>(), L, 0, n, eq.as<Fr>(), lo.as<Fr>(), hi.as<Fr>(), C.stream);
+    if (D.nchunks > 4096) part.alloc(32 * D.nchunks);
+    Fr* o = out.as<Fr>();
+    launch_sparse3(1, D.view(), eq.as<Fr>(), o, nullptr, nullptr, rx.as<Fr>() + L, n, D.chunks.as<LongChunk>(),
+                   D.nchunks, D.lrows.as<LongRow>(), D.nlrows, part.as<Fr>(), C.stream);
+    launch_from_mont(o + n, o, n, C.stream);
+    std::vector<uint8_t> res(32 * n);
+    SPX_HIP(hipMemcpyAsync(res.data(), o + n, 32 * n, hipMemcpyDeviceToHost, C.stream));
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical field element");
+    return res;
+}
+
+std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t* scalars, size_t n) {
+    if (n == 0) invalid("empty MSM");
+    const size_t ps = g2 ? 192 : 96;
+    DevMem raw(ps * n), sc(32 * n), err(sizeof(int));
+    SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
+    SPX_HIP(hipMemcpyAsync(raw.p, bases, ps * n, hipMemcpyHostToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(sc.p, scalars, 32 * n, hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(sc.as<Fr>(), n, err.as<int>(), C.stream);
+    if (g2)
+        launch_points_from_bytes_g2(raw.as<G2Aff>(), n, err.as<int>(), C.stream);
+    else
+        launch_points_from_bytes_g1(raw.as<G1Aff>(), n, err.as<int>(), C.stream);
+    MsmInst I{};
+    I.c = (uint32_t)window_bits_for(n);
+    I.W = (uint32_t)windows_for((int)I.c);
+    I.size = (uint32_t)n;
+    I.stride = (uint32_t)n;
+    DevMem pre(ps * n * I.W), out(4 * (g2 ? sizeof(Fq2) : sizeof(Fq)));
+    if (g2)
+        precompute_level<G2Aff>(C, raw.as<G2Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G2Aff>());
+    else
+        precompute_level<G1Aff>(C, raw.as<G1Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G1Aff>());
+    if (g2)
+        msm_run_g2(C.msm, &I, 1, pre.as<G2Aff>(), sc.as<Fr>(), out.p, C.stream);
+    else
+        msm_run_g1(C.msm, &I, 1, pre.as<G1Aff>(), sc.as<Fr>(), out.p, C.stream);
+    std::vector<uint8_t> h(out.bytes);
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(h.data(), out.p, out.bytes, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical input");
+    std::vector<uint8_t> res(ps);
+    if (g2)
+        host::g2_to_uncompressed(res.data(), xyzz_bytes_to_affine<HFq2>(h.data()));
+    else
+        host::g1_to_uncompressed(res.data(), xyzz_bytes_to_affine<HFq>(h.data()));
+    return res;
+}
+
+std::vector<uint8_t> k_commit(Ctx& C, PP& P, const uint8_t* table, int nv) {
+    if (nv != P.nv) invalid("table size != 2^nv of the public parameters");
+    auto W = witness_upload(C, table, 1, table + 32, (1ull << nv) - 1);
+    Affine<HFq> a = commit_z(C, P, W->z.as<Fr>(), 1ull << nv, 1, 0);
+    std::vector<uint8_t> out(56);
+    uint64_t u = (uint64_t)nv;
+    memcpy(out.data(), &u, 8);
+    host::g1_compress(out.data() + 8, a);
+    return out;
+}
+
+std::vector<uint8_t> k_open(Ctx& C, PP& P, const uint8_t* table, int nv, const uint8_t* point) {
+    if (nv != P.nv) invalid("table size != 2^nv of the public parameters");
+    auto W = witness_upload(C, table, 1, table + 32, (1ull << nv) - 1);
+    std::vector<HFr> pt(nv);
+    for (int i = 0; i < nv; ++i)
+        if (!host::fr_from_bytes(pt[i], point + 32 * i)) throw SpxError(kSerialization, "non-canonical point");
+    OpenOut op = open_z(C, P, W->z.as<Fr>(), nv, pt, 1, 0);
+    Ser s;
+    ser_open(s, op.eval, P, op.proofs);
+    return s.b;
+}
+
+}  // namespace spx

@@ -1,0 +1,212 @@
+// Host-side state of the MI355X prover: contexts (one per GPU / rank), communicators,
+// device-resident public parameters, prover keys, witnesses.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "host_ff.hpp"
+#include "kernels.hpp"
+#include "transcript.hpp"
+
+namespace spx {
+
+struct SpxError : std::runtime_error {
+    int code;
+    SpxError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+enum { kOk = 0, kInvalidArgument = 1, kSumcheck = 2, kWrongWitness = 3, kSerialization = 4, kDevice = 5 };
+
+#define SPX_HIP(x)                                                                                   \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess)                                                                        \
+            throw ::spx::SpxError(::spx::kDevice, std::string("HIP: ") + hipGetErrorString(e_) + " (" #x ") at " + \
+                                                     __FILE__ + ":" + std::to_string(__LINE__));    \
+    } while (0)
+
+inline void invalid(const std::string& m) { throw SpxError(kInvalidArgument, m); }
+
+// owning device allocation
+struct DevMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevMem() = default;
+    explicit DevMem(size_t b) { alloc(b); }
+    void alloc(size_t b) {
+        release();
+        if (b) SPX_HIP(hipMalloc(&p, b));
+        bytes = b;
+    }
+    void ensure(size_t b) {
+        if (b > bytes) alloc(b);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    ~DevMem() { release(); }
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+};
+
+// ---------------------------------------------------------------- communicators
+struct Comm {
+    virtual ~Comm() {}
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    // host buffers; every rank contributes `bytes`, recv holds size() * bytes in rank order
+    virtual void allgather(const void* send, void* recv, size_t bytes) = 0;
+};
+struct LocalComm : Comm {
+    int rank() const override { return 0; }
+    int size() const override { return 1; }
+    void allgather(const void* s, void* r, size_t b) override { memcpy(r, s, b); }
+};
+struct GroupState {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::vector<uint8_t>> slots;
+    int arrived = 0;
+    uint64_t gen = 0;
+    explicit GroupState(int w) : world(w), slots(w) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+struct GroupComm : Comm {
+    std::shared_ptr<GroupState> st;
+    int r;
+    GroupComm(std::shared_ptr<GroupState> s, int rk) : st(std::move(s)), r(rk) {}
+    int rank() const override { return r; }
+    int size() const override { return st->world; }
+    void allgather(const void* s, void* rv, size_t b) override {
+        {
+            std::lock_guard<std::mutex> lk(st->mu);
+            st->slots[r].assign((const uint8_t*)s, (const uint8_t*)s + b);
+        }
+        st->barrier();
+        for (int k = 0; k < st->world; ++k) memcpy((uint8_t*)rv + k * b, st->slots[k].data(), b);
+        st->barrier();
+    }
+};
+std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int rank, int world, int device, hipStream_t s);
+
+// ---------------------------------------------------------------- context
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    MsmWorkspace* msm = nullptr;
+    std::unique_ptr<Comm> comm;
+    // pinned staging
+    uint8_t* pin = nullptr;
+    size_t pin_bytes = 0;
+    // per-prove scratch
+    DevMem scratch;
+    std::vector<std::pair<std::string, double>> timings;
+    Ctx(int dev);
+    ~Ctx();
+    uint8_t* pinned(size_t b);
+    void sync() { SPX_HIP(hipStreamSynchronize(stream)); }
+};
+
+// ---------------------------------------------------------------- public parameters
+struct PP {
+    int nv = 0;
+    DevMem g1_raw_mem, g2_raw_mem;            // all levels, contiguous
+    std::vector<uint64_t> lvl_off;            // point offset of level i (2^(nv-i) points)
+    host::Affine<host::Fq> g;
+    host::Affine<host::Fq2> h;
+    // window copies (device, affine): commit bases (level 0 of G1)
+    DevMem g1_pre;
+    int g1_c = 0, g1_W = 0;
+    // G2 opening bases: level i pair-summed (2^(nv-i-1) points), copies [W_i][size_i]
+    DevMem g2_pre;
+    std::vector<uint64_t> g2_off;
+    std::vector<int> g2_c, g2_W;
+    bool has_t = false;
+    std::vector<host::Fr> t;  // trapdoor (keygen only; tests)
+    G1Aff* g1_level(int i) const { return g1_raw_mem.as<G1Aff>() + lvl_off[i]; }
+    G2Aff* g2_level(int i) const { return g2_raw_mem.as<G2Aff>() + lvl_off[i]; }
+};
+void pp_preprocess(Ctx& C, PP& P);
+int window_bits_for(uint64_t size);
+
+// ---------------------------------------------------------------- index
+struct HostCsr {
+    uint64_t n = 0;
+    std::vector<uint64_t> rp;
+    std::vector<uint32_t> col;
+    std::vector<uint8_t> val;  // canonical bytes
+};
+struct DevSparse {  // rank-local block of 3 matrices (CSR rows or CSC columns)
+    DevMem ptr[3], idx[3], val[3];
+    DevMem chunks, lrows;
+    int nchunks = 0, nlrows = 0;
+    SparseView3 view() const {
+        SparseView3 v;
+        for (int m = 0; m < 3; ++m) {
+            v.ptr[m] = ptr[m].as<uint64_t>();
+            v.idx[m] = idx[m].as<uint32_t>();
+            v.val[m] = val[m].as<Fr>();
+        }
+        return v;
+    }
+};
+struct Index {
+    int log_n = 0;
+    uint64_t n = 0;
+    HostCsr m[3];
+    DevSparse rows, cols;  // local rows (SpMV), local columns (eval_on_x)
+    bool has_cache = false;
+    Blake2s cache;  // transcript state after feeding A, B, C
+    int G = 1, rank = 0;
+};
+
+struct Witness {
+    uint64_t n = 0;
+    std::vector<uint8_t> v;  // canonical bytes (transcript)
+    DevMem z;                // Montgomery, full n
+};
+
+struct ProveOpts {
+    int mode = 0;
+    uint64_t seed = 0;
+    bool cached = false;
+};
+
+// entry points used by the C ABI
+std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len);
+std::unique_ptr<PP> pp_generate(Ctx& C, int nv, uint64_t seed);
+std::vector<uint8_t> pp_serialize(Ctx& C, const PP& P);
+std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats);
+std::unique_ptr<Witness> witness_upload(Ctx& C, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw);
+std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts& o);
+size_t proof_size(int log_n);
+
+std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z);
+std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x);
+std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t* scalars, size_t n);
+std::vector<uint8_t> k_commit(Ctx& C, PP& P, const uint8_t* table, int nv);
+std::vector<uint8_t> k_open(Ctx& C, PP& P, const uint8_t* table, int nv, const uint8_t* point);
+
+}  // namespace spx

@@ -99,6 +99,37 @@ int spx_prove_witness(spx_ctx *ctx, spx_pk *idx, spx_witness *wit, spx_pp *pp, c
 /* per-phase device timings of the last prove on this ctx, microseconds */
 int spx_last_timings(spx_ctx *ctx, double *out, int cap, int *n);
 
+/* ---- synthetic instances (SURVEY §8(d) generators; SplitMix64, same draws as the test oracle) ----
+ * kind 0 = uniform-3n (satisfiable, nnz = 3n), 1 = ref-shaped (TestSynthesizer, param = density).
+ * spx_synth_csr fills views into the handle (valid until spx_synth_free). */
+typedef struct spx_synth spx_synth;
+int spx_synth_create(int kind, int log_n, int log_v, uint64_t seed, uint64_t param, spx_synth **out);
+uint64_t spx_synth_nnz(const spx_synth *s, int m);
+int spx_synth_csr(const spx_synth *s, int m, spx_csr *out);
+const uint8_t *spx_synth_z(const spx_synth *s);
+int spx_synth_free(spx_synth *s);
+
+/* ---- live kernel statistics (HIP events on the library's stream, enabled per ctx) ----
+ * ids: see SPX_K_* below; per id: launches, summed device ms, summed algorithmic bytes. */
+enum {
+    SPX_K_SC1 = 0,      /* sumcheck #1 round (fold + evaluate) */
+    SPX_K_SC2 = 1,      /* sumcheck #2 round */
+    SPX_K_SPMV = 2,     /* Az, Bz, Cz */
+    SPX_K_MTV = 3,      /* sum_m r_m M(r_x, .) */
+    SPX_K_OPEN = 4,     /* mKZG quotient / fold level */
+    SPX_K_EQ = 5,       /* eq tables */
+    SPX_K_MSM_SORT = 6, /* digit count + scatter (both curves) */
+    SPX_K_ACC_G1 = 7,   /* bucket accumulation, affine level, G1 */
+    SPX_K_ACC_G2 = 8,   /* bucket accumulation, affine level, G2 */
+    SPX_K_ACCX_G1 = 9,  /* bucket accumulation, XYZZ levels, G1 */
+    SPX_K_ACCX_G2 = 10, /* bucket accumulation, XYZZ levels, G2 */
+    SPX_K_RED_G1 = 11,  /* bucket weighting + final reduction, G1 */
+    SPX_K_RED_G2 = 12,  /* bucket weighting + final reduction, G2 */
+    SPX_K_COUNT = 13
+};
+int spx_kernel_stats_enable(spx_ctx *ctx, int on);
+int spx_kernel_stats(spx_ctx *ctx, int id, uint64_t *launches, double *ms, double *bytes);
+
 /* ---- kernel-level entry points (parity tests) ---- */
 int spx_sum_over_y(spx_ctx *ctx, const spx_csr *m, const uint8_t *z, uint8_t *out);
 int spx_eval_on_x(spx_ctx *ctx, const spx_csr *m, const uint8_t *r_x, uint8_t *out);

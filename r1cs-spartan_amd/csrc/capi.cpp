@@ -59,6 +59,7 @@ spx::HostCsr to_host(const spx_csr* m) {
 void set_dev(spx_ctx* c) {
     if (!c) spx::invalid("null context");
     SPX_HIP(hipSetDevice(c->c->device));
+    spx::g_kprof = &c->c->kprof;  // kernel statistics of this ctx for the calling thread
 }
 spx::ProveOpts opts_of(const spx_prove_opts* o) {
     spx::ProveOpts p;
@@ -202,6 +203,26 @@ int spx_last_timings(spx_ctx* ctx, double* out, int cap, int* n) {
         auto& t = ctx->c->timings;
         if (n) *n = (int)t.size();
         for (int i = 0; i < (int)t.size() && i < cap; ++i) out[i] = t[i].second;
+    });
+}
+
+int spx_kernel_stats_enable(spx_ctx* ctx, int on) {
+    return guard([&] {
+        set_dev(ctx);
+        ctx->c->sync();
+        ctx->c->kprof.on = on != 0;
+        ctx->c->kprof.reset();
+    });
+}
+int spx_kernel_stats(spx_ctx* ctx, int id, uint64_t* launches, double* ms, double* bytes) {
+    return guard([&] {
+        if (id < 0 || id >= SPX_K_COUNT) spx::invalid("bad kernel id");
+        set_dev(ctx);
+        ctx->c->sync();
+        auto& k = ctx->c->kprof;
+        if (launches) *launches = k.launches[id];
+        if (ms) *ms = k.ms[id];
+        if (bytes) *bytes = k.bytes[id];
     });
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "curve_dev.hpp"
 
 namespace spx {
@@ -31,6 +33,70 @@ struct LongRow {
 struct Tables3 {
     Fr* t[3];
 };
+
+// ---- live kernel statistics (HIP events around selected launches; off unless enabled)
+struct KProf {
+    bool on = false;
+    struct Rec {
+        int id;
+        hipEvent_t a, b;
+        double bytes;
+    };
+    std::vector<Rec> open;  // recorded, not yet harvested
+    std::vector<hipEvent_t> pool;
+    uint64_t launches[16] = {0};
+    double ms[16] = {0}, bytes[16] = {0};
+    int cur_id = -1;
+    hipEvent_t cur_a = nullptr;
+    hipEvent_t get() {
+        if (pool.empty()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            return e;
+        }
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    void begin(int id, hipStream_t s) {
+        if (!on) return;
+        cur_id = id;
+        cur_a = get();
+        (void)hipEventRecord(cur_a, s);
+    }
+    void end(double algo_bytes, hipStream_t s) {
+        if (!on || cur_id < 0) return;
+        hipEvent_t b = get();
+        (void)hipEventRecord(b, s);
+        open.push_back({cur_id, cur_a, b, algo_bytes});
+        cur_id = -1;
+    }
+    void harvest() {  // call after a stream sync
+        for (auto& r : open) {
+            float t = 0;
+            if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+                launches[r.id] += 1;
+                ms[r.id] += t;
+                bytes[r.id] += r.bytes;
+            }
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        open.clear();
+    }
+    void reset() {
+        for (int i = 0; i < 16; ++i) launches[i] = 0, ms[i] = 0, bytes[i] = 0;
+    }
+};
+extern thread_local KProf* g_kprof;  // set by the host for the calling thread
+inline void kp_begin(int id, hipStream_t s) {
+    if (g_kprof) g_kprof->begin(id, s);
+}
+inline void kp_end(double bytes, hipStream_t s) {
+    if (g_kprof) g_kprof->end(bytes, s);
+}
+enum { KP_SC1 = 0, KP_SC2, KP_SPMV, KP_MTV, KP_OPEN, KP_EQ, KP_SORT, KP_ACC_G1, KP_ACC_G2, KP_ACCX_G1, KP_ACCX_G2,
+       KP_RED_G1, KP_RED_G2 };
 
 // ---- mle_kernels.hip
 void launch_to_mont(Fr* d, size_t n, int* err, hipStream_t s);

@@ -13,6 +13,7 @@
 
 namespace spx {
 
+thread_local KProf* g_kprof = nullptr;
 static constexpr int kThreads = 256;
 
 DEV Fr ld_fr(const Fr* p) {
@@ -389,8 +390,10 @@ void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* 
     int klo = (k + 1) / 2, khi = k - klo;
     hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev, klo, scratch_lo);
     hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev + klo, khi, scratch_hi);
+    kp_begin(KP_EQ, s);
     hipLaunchKernelGGL(k_eq_expand, dim3(grid_for(count, 8192)), dim3(kThreads), 0, s, scratch_lo, scratch_hi, klo, base,
                        count, out);
+    kp_end(32.0 * (double)count, s);
 }
 
 int sc_grid(uint64_t half) { return grid_for(half, 1024); }
@@ -398,25 +401,32 @@ int sc_grid(uint64_t half) { return grid_for(half, 1024); }
 void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr* r,
                       uint64_t half, Fr* partial, Fr* result3, hipStream_t s) {
     int g = sc_grid(half);
+    kp_begin(KP_SC1, s);
     if (fold)
         hipLaunchKernelGGL(k_sc1_round<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
     else
         hipLaunchKernelGGL(k_sc1_round<false>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
+    // algorithmic bytes: fold reads 4 Fr x 3 tables + 2 E, writes 2 x 3 + 1 E; no fold reads 2 x 3 + 1
+    kp_end(32.0 * (double)half * (fold ? (14.0 + 6.0 + (Eout ? 1.0 : 0.0)) : 7.0), s);
     hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
 void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr* r, uint64_t half,
                       Fr* partial, Fr* result3, hipStream_t s) {
     int g = sc_grid(half);
+    kp_begin(KP_SC2, s);
     if (fold)
         hipLaunchKernelGGL(k_sc2_round<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
     else
         hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
+    kp_end(32.0 * (double)half * (fold ? 12.0 : 4.0), s);
     hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s) {
+    kp_begin(KP_OPEN, s);
     hipLaunchKernelGGL(k_open_level, dim3(grid_for(half, 8192)), dim3(kThreads), 0, s, rin, rout, q, point, half);
+    kp_end(32.0 * 4.0 * (double)half, s);  // read 2, write q and r'
 }
 
 }  // namespace spx

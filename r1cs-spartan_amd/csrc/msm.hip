@@ -308,12 +308,17 @@ static void msm_run(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>
 
     HIPCHK(hipMemsetAsync(counts, 0, 4 * (nb + 1), s));
     const int gsc = (int)((tot_sc + kLight - 1) / kLight);
+    const bool g2 = sizeof(F) == sizeof(Fq2);
+    kp_begin(KP_SORT, s);
     hipLaunchKernelGGL(k_msm_digits<false>, dim3(gsc), dim3(kLight), 0, s, d_insts, d_prefix, ninst, tot_sc, scalars,
                        counts, nullptr, nullptr);
+    kp_end(32.0 * tot_sc, s);
     exclusive_scan(ws, counts, offs, nb + 1, s);
     HIPCHK(hipMemcpyAsync(cursor, offs, 4 * (nb + 1), hipMemcpyDeviceToDevice, s));
+    kp_begin(KP_SORT, s);
     hipLaunchKernelGGL(k_msm_digits<true>, dim3(gsc), dim3(kLight), 0, s, d_insts, d_prefix, ninst, tot_sc, scalars,
                        nullptr, cursor, refs);
+    kp_end(32.0 * tot_sc + 4.0 * tot_refs, s);
     {
         size_t tb = 0;
         HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, counts, d_max, nb, s));
@@ -332,8 +337,11 @@ static void msm_run(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>
     const int gb = (int)((nb + 1 + kLight - 1) / kLight);
     hipLaunchKernelGGL(k_seg_counts, dim3(gb), dim3(kLight), 0, s, counts, nb, segcnt);
     exclusive_scan(ws, segcnt, soa, nb + 1, s);
+    kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((max_segs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, soa,
                        nb, offs, counts, refs, pts, PA);
+    // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
+    kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg) * psz, s);
     // the per-bucket counts of PA are segcnt, offsets soa
     uint32_t* cur_cnt = segcnt;
     uint32_t* cur_off = soa;
@@ -347,8 +355,10 @@ static void msm_run(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>
         hipLaunchKernelGGL(k_seg_counts, dim3(gb), dim3(kLight), 0, s, cur_cnt, nb, spare_cnt);
         exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
+        kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
         hipLaunchKernelGGL(k_accum_xyzz<F>, dim3((unsigned)((nsegs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
                            nxt_off, nb, cur_off, cur_cnt, cur, nxt);
+        kp_end((double)(cur_max_segs + nsegs) * psz, s);
         std::swap(cur, nxt);
         std::swap(cur_off, nxt_off);
         std::swap(cur_cnt, spare_cnt);
@@ -357,9 +367,11 @@ static void msm_run(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>
     }
     // weighting
     auto* red = (Xyzz<F>*)ws->red.ensure(psz * std::max<uint64_t>(tot_red, 1));
+    kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     hipLaunchKernelGGL(k_bucket_reduce<F>, dim3((unsigned)((tot_red + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
                        d_insts, d_redp, ninst, tot_red, cur_cnt, cur_off, cur, red);
     hipLaunchKernelGGL(k_final_reduce<F>, dim3(ninst), dim3(64), 0, s, d_insts, red, (Xyzz<F>*)out_dev);
+    kp_end((double)nb * psz, s);
     HIPCHK(hipGetLastError());
 }
 

@@ -444,6 +444,15 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
         rps[m] = std::move(cp);
     }
     upload_sparse(C, I->cols, rps, cols, vals, lo, nl, err.as<int>());
+    {
+        double e_rows = 0, e_cols = 0;
+        for (int m = 0; m < 3; ++m) {
+            e_rows += (double)(mats[m].rp[lo + nl] - mats[m].rp[lo]);
+            e_cols += (double)(rps[m][lo + nl] - rps[m][lo]);
+        }
+        I->rows_bytes = 68.0 * e_rows + 3.0 * 8.0 * nl + 3.0 * 32.0 * nl;  // 3 outputs
+        I->cols_bytes = 68.0 * e_cols + 3.0 * 8.0 * nl + 32.0 * nl;        // 1 combined output
+    }
     int herr = 0;
     SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
     C.sync();
@@ -752,8 +761,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     // ---- SpMV Az, Bz, Cz (challenge-independent: queued first, overlaps the commit's host work)
     {
         SparseView3 rv = I.rows.view();
+        kp_begin(KP_SPMV, C.stream);
         launch_sparse3(0, rv, z, Az, Bz, Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(), I.rows.nchunks,
                        I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
+        kp_end(I.rows_bytes, C.stream);
     }
     // ---- round 1: commitment (prover.rs:123-141)
     Affine<HFq> com = commit_z(C, P, z, n, G, rank);
@@ -911,8 +922,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     launch_eq_table(rxdev, L, 0, n, EQ, eqlo, eqhi, C.stream);
     {
         SparseView3 cv = I.cols.view();
+        kp_begin(KP_MTV, C.stream);
         launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, rxdev + L, nl, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
                        I.cols.lrows.as<LongRow>(), I.cols.nlrows, partial, C.stream);
+        kp_end(I.cols_bytes, C.stream);
     }
     {
         size_t m0 = proof.b.size();

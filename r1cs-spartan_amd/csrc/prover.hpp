@@ -123,10 +123,14 @@ struct Ctx {
     // per-prove scratch
     DevMem scratch;
     std::vector<std::pair<std::string, double>> timings;
+    KProf kprof;
     Ctx(int dev);
     ~Ctx();
     uint8_t* pinned(size_t b);
-    void sync() { SPX_HIP(hipStreamSynchronize(stream)); }
+    void sync() {
+        SPX_HIP(hipStreamSynchronize(stream));
+        if (kprof.on) kprof.harvest();
+    }
 };
 
 // ---------------------------------------------------------------- public parameters
@@ -179,6 +183,7 @@ struct Index {
     DevSparse rows, cols;  // local rows (SpMV), local columns (eval_on_x)
     bool has_cache = false;
     Blake2s cache;  // transcript state after feeding A, B, C
+    double rows_bytes = 0, cols_bytes = 0;  // algorithmic bytes of one SpMV / eval_on_x pass (local)
     int G = 1, rank = 0;
 };
 

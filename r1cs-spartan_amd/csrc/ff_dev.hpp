@@ -152,9 +152,10 @@ DEV void fe_dbl(Fe<C>& r, const Fe<C>& a) {
     fe_add(r, a, a);
 }
 
-// Montgomery multiplication, CIOS, 32-bit limbs.
+// Montgomery multiplication, CIOS, 32-bit limbs (portable form; the asm product-scanning form in
+// ff_asm.hpp is the one the kernels use).
 template <class C>
-DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
+DEV void fe_mul_cios(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
     constexpr int N = C::N;
     uint32_t t[N + 1];
 #pragma unroll
@@ -187,6 +188,20 @@ DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
     for (int i = 0; i < N; ++i) res[i] = t[i];
     fe_reduce_once<C>(r, res);
+}
+
+#include "ff_asm.hpp"
+
+template <class C>
+DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
+#ifdef SPX_NO_ASM_MUL
+    fe_mul_cios(r, a, b);
+#else
+    if constexpr (C::N == 8)
+        fr_mul_asm(r, a, b);
+    else
+        fq_mul_asm(r, a, b);
+#endif
 }
 
 template <class C>

@@ -1,0 +1,218 @@
+// Pippenger multi-scalar multiplication for G1 (commit, commit.rs:25) and G2 (opening proofs,
+// open.rs:49), plus the public-parameter preprocessing and fixed-base keygen kernels.
+//
+// Design (MI355X-first, HBM capacity traded for latency):
+//  * PP preprocessing stores, for every base B_j, the W window copies 2^(c w) B_j as affine
+//    points, so all windows of an MSM share ONE set of 2^(c-1) signed-digit buckets and no
+//    window-combination doubling chain is ever run (that chain is a ~255-step serial dependency
+//    on a single lane). G2 bases of open level i are pre-summed pairs raw[2b] + raw[2b+1],
+//    because open.rs:46 feeds every quotient scalar twice (q_k[x >> 1]); the MSM result is
+//    identical and half the size.
+//  * Signed c-bit digits -> counting sort by bucket (atomic histogram, hipCUB scan, atomic
+//    scatter of 32-bit point references with the sign in bit 31). Order inside a bucket is
+//    irrelevant: group addition is exact and commutative, the affine result is unique.
+//  * Bucket accumulation in XYZZ coordinates over fixed segments of kSeg references per thread
+//    (load-balanced whatever the scalar distribution), repeated on the partial sums until every
+//    bucket has one value (log_kSeg(max bucket) levels: one host sync to read the max count).
+//  * Bucket weighting sum_j j S_j with per-thread running sums over L buckets plus one small
+//    scalar multiple, then a per-instance block reduction. Result: one XYZZ point per MSM.
+// Many MSMs run as one batch (all nv levels of an opening): one pipeline, one sync.
+#include "msm_common.hpp"
+
+namespace spx {
+
+__device__ __constant__ constexpr uint32_t kFqR2[12] = {0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u,
+                                                       0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, 0x67eb88a9u,
+                                                       0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u};
+
+// ------------------------------------------------------------------ digits: count / scatter
+template <bool SCATTER>
+__global__ __launch_bounds__(kLight) void k_msm_digits(const MsmInst* __restrict__ insts,
+                                                       const uint64_t* __restrict__ prefix, int ninst,
+                                                       uint64_t total, const Fr* __restrict__ scalars,
+                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ cursor,
+                                                       uint32_t* __restrict__ refs) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int i = find_slot(prefix, ninst, g);
+    const uint64_t j = g - prefix[i];
+    const MsmInst I = insts[i];
+    Fr m, s;
+    load_vec(m, scalars + I.scalar_off + j);
+    fe_from_mont(s, m);
+    const uint32_t c = I.c, full = 1u << c, half = full >> 1, mask = full - 1;
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < I.W; ++w) {
+        uint32_t v = (s.v[0] & mask) + carry;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
+        s.v[7] >>= c;
+        int32_t d;
+        if (v > half) {
+            d = (int32_t)v - (int32_t)full;
+            carry = 1;
+        } else {
+            d = (int32_t)v;
+            carry = 0;
+        }
+        if (d != 0) {
+            const uint32_t b = I.bucket_off + (uint32_t)(d < 0 ? -d : d) - 1;
+            if (!SCATTER) {
+                atomicAdd(&counts[b], 1u);
+            } else {
+                const uint32_t pos = atomicAdd(&cursor[b], 1u);
+                refs[pos] = (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
+            }
+        }
+    }
+}
+
+__global__ void k_seg_counts(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t* __restrict__ segcnt,
+                             uint32_t seg) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) segcnt[b] = (cnt[b] + seg - 1) / seg;
+    if (b == nb) segcnt[b] = 0;
+}
+
+
+void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s) {
+    const int gb = (int)((nb + 1 + kLight - 1) / kLight);
+    hipLaunchKernelGGL(k_seg_counts, dim3(gb), dim3(kLight), 0, s, cnt, nb, segcnt, seg);
+}
+
+MsmWorkspace* msm_ws_create() { return new MsmWorkspace(); }
+void msm_ws_destroy(MsmWorkspace* ws) { delete ws; }
+
+void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
+    void* t = ws->cub.ensure(tb);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
+}
+
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s) {
+    MsmSorted o;
+    o.insts.assign(ih, ih + ninst);
+    std::vector<uint64_t> prefix(ninst + 1);
+    uint64_t tot_sc = 0, tot_refs = 0;
+    uint32_t nb = 0;
+    for (int i = 0; i < ninst; ++i) {
+        MsmInst& I = o.insts[i];
+        I.bucket_off = nb;
+        nb += 1u << (I.c - 1);
+        prefix[i] = tot_sc;
+        tot_sc += I.size;
+        tot_refs += (uint64_t)I.size * I.W;
+    }
+    prefix[ninst] = tot_sc;
+    if (tot_refs >= 0xffffffffull) throw std::runtime_error("MSM batch too large");
+    o.nb = nb;
+    o.tot_refs = tot_refs;
+    o.d_insts = (MsmInst*)ws->insts.ensure(sizeof(MsmInst) * ninst);
+    auto* d_prefix = (uint64_t*)ws->prefix.ensure(8 * (ninst + 1));
+    HIPCHK(hipMemcpyAsync(o.d_insts, o.insts.data(), sizeof(MsmInst) * ninst, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_prefix, prefix.data(), 8 * (ninst + 1), hipMemcpyHostToDevice, s));
+    o.counts = (uint32_t*)ws->counts.ensure(4 * (nb + 1));
+    o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
+    uint32_t* cursor = (uint32_t*)ws->cursor.ensure(4 * (nb + 1));
+    o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(tot_refs, 1));
+    o.segcnt = (uint32_t*)ws->segcnt.ensure(4 * (nb + 1));
+    o.soa = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
+    o.sob = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
+    o.spare = cursor;
+    auto* d_max = (uint32_t*)ws->maxv.ensure(4);
+    HIPCHK(hipMemsetAsync(o.counts, 0, 4 * (nb + 1), s));
+    if (tot_sc) {
+        const int gsc = (int)((tot_sc + kLight - 1) / kLight);
+        kp_begin(KP_SORT, s);
+        hipLaunchKernelGGL(k_msm_digits<false>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, ninst, tot_sc,
+                           scalars, o.counts, nullptr, nullptr);
+        kp_end(32.0 * tot_sc, s);
+        exclusive_scan(ws, o.counts, o.offs, nb + 1, s);
+        HIPCHK(hipMemcpyAsync(cursor, o.offs, 4 * (nb + 1), hipMemcpyDeviceToDevice, s));
+        kp_begin(KP_SORT, s);
+        hipLaunchKernelGGL(k_msm_digits<true>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, ninst, tot_sc,
+                           scalars, nullptr, cursor, o.refs);
+        kp_end(32.0 * tot_sc + 4.0 * tot_refs, s);
+    } else {
+        exclusive_scan(ws, o.counts, o.offs, nb + 1, s);
+    }
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, o.counts, d_max, nb, s));
+    void* t = ws->cub.ensure(tb);
+    HIPCHK(hipcub::DeviceReduce::Max(t, tb, o.counts, d_max, nb, s));
+    HIPCHK(hipMemcpyAsync(ws->h_max, d_max, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    o.maxc = *ws->h_max;
+    return o;
+}
+
+// ------------------------------------------------------------------ byte images <-> device points
+DEV bool fq_canon_to_mont(Fq& r, const Fq& c) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        uint64_t d = (uint64_t)c.v[i] - kFqP[i] - br;
+        br = (uint32_t)(d >> 63);
+    }
+    Fq r2;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r2.v[i] = kFqR2[i];
+    fe_mul(r, c, r2);
+    return br != 0;  // c < q
+}
+
+template <int NF>  // NF = number of Fq coordinates per point (2 for G1, 4 for G2)
+__global__ void k_points_from_bytes(Fq* pts, uint64_t n, int* err) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        Fq* p = pts + j * NF;
+        Fq last;
+        load_vec(last, p + NF - 1);
+        const uint32_t flags = last.v[11] >> 30;
+        bool ok = true;
+        if (flags & 1u) {  // bit 6 of the last byte: point at infinity
+            Fq z;
+            fe_zero(z);
+#pragma unroll
+            for (int k = 0; k < NF; ++k) store_vec(p + k, z);
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+            Fq c, m;
+            load_vec(c, p + k);
+            if (k == NF - 1) c.v[11] &= 0x3fffffffu;
+            ok &= fq_canon_to_mont(m, c);
+            store_vec(p + k, m);
+        }
+        if (!ok) atomicOr(err, 1);
+    }
+}
+template <int NF>
+__global__ void k_points_to_canon(Fq* pts, uint64_t n) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        Fq* p = pts + j * NF;
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+            Fq m, c;
+            load_vec(m, p + k);
+            fe_from_mont(c, m);
+            store_vec(p + k, c);
+        }
+    }
+}
+static unsigned pgrid(uint64_t n) { return (unsigned)std::min<uint64_t>((n + 255) / 256, 8192); }
+void launch_points_from_bytes_g1(G1Aff* pts, uint64_t n, int* err, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_points_from_bytes<2>, dim3(pgrid(n)), dim3(256), 0, s, (Fq*)pts, n, err);
+}
+void launch_points_from_bytes_g2(G2Aff* pts, uint64_t n, int* err, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_points_from_bytes<4>, dim3(pgrid(n)), dim3(256), 0, s, (Fq*)pts, n, err);
+}
+void launch_points_to_canon_g1(G1Aff* pts, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_points_to_canon<2>, dim3(pgrid(n)), dim3(256), 0, s, (Fq*)pts, n);
+}
+void launch_points_to_canon_g2(G2Aff* pts, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_points_to_canon<4>, dim3(pgrid(n)), dim3(256), 0, s, (Fq*)pts, n);
+}
+
+}  // namespace spx

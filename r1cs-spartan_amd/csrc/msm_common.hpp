@@ -1,0 +1,102 @@
+// Shared pieces of the MSM translation units (msm_common.hip, msm_g1.hip, msm_g2.hip).
+#pragma once
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace spx {
+
+static constexpr uint32_t kSeg1 = 32;  // references per thread, affine accumulation level
+static constexpr uint32_t kSeg = 32;    // partials per thread, XYZZ accumulation levels
+static constexpr int kLight = 256;  // threads for bookkeeping kernels
+static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
+
+#define HIPCHK(x)                                                                                     \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + \
+                                                       " at " __FILE__ ":" + std::to_string(__LINE__)); \
+    } while (0)
+
+// ------------------------------------------------------------------ helpers
+template <class F>
+DEV bool aff_is_sentinel(const Aff<F>& a) {
+    return FieldOps<F>::is_zero(a.x) && FieldOps<F>::is_zero(a.y);
+}
+template <class F>
+DEV void aff_set_sentinel(Aff<F>& a) {
+    FieldOps<F>::zero(a.x);
+    FieldOps<F>::zero(a.y);
+}
+
+DEV int find_slot(const uint64_t* prefix, int n, uint64_t g) {  // largest i with prefix[i] <= g
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (prefix[mid] <= g)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+DEV uint32_t find_bucket(const uint32_t* off, uint32_t nb, uint32_t s) {  // largest b with off[b] <= s
+    uint32_t lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= s)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* ensure(size_t bytes) {
+        if (bytes > cap) {
+            if (p) HIPCHK(hipFree(p));
+            size_t nb = std::max(bytes, cap + cap / 2);
+            HIPCHK(hipMalloc(&p, nb));
+            cap = nb;
+        }
+        return p;
+    }
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct MsmWorkspace {
+    DBuf insts, prefix, redp, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, maxv,
+        tprefix;
+    uint32_t* h_max = nullptr;
+    MsmWorkspace() { HIPCHK(hipHostMalloc((void**)&h_max, sizeof(uint32_t))); }
+    ~MsmWorkspace() {
+        if (h_max) (void)hipHostFree(h_max);
+    }
+};
+
+void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
+
+// Result of the digit / counting-sort stage of a batch (device pointers into the workspace).
+struct MsmSorted {
+    uint32_t nb = 0;          // buckets in the batch
+    uint64_t tot_refs = 0;    // (scalar, window) references with a non-zero digit (upper bound: size * W)
+    uint32_t maxc = 0;        // largest bucket
+    uint32_t *counts, *offs, *refs, *segcnt, *soa, *sob, *spare;
+    MsmInst* d_insts;
+    std::vector<MsmInst> insts;  // host copy with bucket offsets filled in
+};
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s);
+void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s);
+
+}  // namespace spx

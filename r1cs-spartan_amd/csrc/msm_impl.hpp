@@ -1,0 +1,377 @@
+// Curve-templated MSM kernels and drivers; instantiated once per curve (msm_g1.hip, msm_g2.hip)
+// so the heavy big-integer code of G1 and G2 compiles in parallel.
+#pragma once
+#include "msm_common.hpp"
+
+namespace spx {
+
+// ------------------------------------------------------------------ accumulation levels
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict__ segoff, uint32_t nb,
+                                                      const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ cnt,
+                                                      const uint32_t* __restrict__ refs,
+                                                      const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= segoff[nb]) return;
+    const uint32_t b = find_bucket(segoff, nb, s);
+    const uint32_t k = s - segoff[b];
+    const uint32_t start = off[b] + k * kSeg1;
+    const uint32_t end = min(start + kSeg1, off[b] + cnt[b]);
+    Xyzz<F> acc;
+    xyzz_set_inf(acc);
+    for (uint32_t e = start; e < end; ++e) {
+        const uint32_t r = refs[e];
+        Aff<F> p;
+        load_vec(p, pts + (r & 0x7fffffffu));
+        if (aff_is_sentinel(p)) continue;
+        xyzz_madd(acc, p, (r >> 31) != 0);
+    }
+    store_vec(out + s, acc);
+}
+
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restrict__ segoff, uint32_t nb,
+                                                       const uint32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ cnt,
+                                                       const Xyzz<F>* __restrict__ in, Xyzz<F>* __restrict__ out) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= segoff[nb]) return;
+    const uint32_t b = find_bucket(segoff, nb, s);
+    const uint32_t k = s - segoff[b];
+    const uint32_t start = off[b] + k * kSeg;
+    const uint32_t end = min(start + kSeg, off[b] + cnt[b]);
+    Xyzz<F> acc;
+    load_vec(acc, in + start);
+    for (uint32_t e = start + 1; e < end; ++e) {
+        Xyzz<F> p;
+        load_vec(p, in + e);
+        xyzz_add(acc, p);
+    }
+    store_vec(out + s, acc);
+}
+
+// ------------------------------------------------------------------ bucket weighting: low-depth tree
+// Result = sum_j (j+1) S_j over the B = 2^(c-1) bucket sums of an instance. Binary tree over the
+// buckets; node = (F, S, D) with F = sum_m (m+1) X_m (local index m), S = sum X_m, D = size * S:
+//   parent(l, r) = (F_l + D_r + F_r,  S_l + S_r,  2 (D_l + D_r))      (size(l) = size(r))
+// One level per launch, one thread per (node, component), component-major so every wave runs one
+// component (no divergence between the F / S / D formulas): the dependent depth is 2 group
+// operations per level (~2 log2 B in total) instead of a per-thread running sum over many
+// buckets — single-lane latency of a G2 addition is ~100 us on CDNA4, so depth is what matters.
+// A missing right child (instances with fewer buckets) is the point at infinity: F and S pass
+// through unchanged, so all instances of a batch run the same number of levels.
+template <class F>
+DEV void ld_bucket(Xyzz<F>& x, uint32_t b, const uint32_t* cnt, const uint32_t* off, const Xyzz<F>* P) {
+    if (cnt[b])
+        load_vec(x, P + off[b]);
+    else
+        xyzz_set_inf(x);
+}
+
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_tree_leaf(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp,
+                                                      int ninst, const uint32_t* __restrict__ node_off,
+                                                      const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                                                      const Xyzz<F>* __restrict__ P, Xyzz<F>* __restrict__ Fo,
+                                                      Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t N = wp[ninst];  // output nodes; component-major so a wave runs one component
+    if (t >= 3 * N) return;
+    const uint32_t comp = (uint32_t)(t / N);
+    const uint64_t tn = t - comp * N;
+    const int i = find_slot(wp, ninst, tn);
+    const uint32_t k = (uint32_t)(tn - wp[i]);
+    const MsmInst I = insts[i];
+    Xyzz<F> l, r;
+    ld_bucket(l, I.bucket_off + 2 * k, cnt, off, P);
+    ld_bucket(r, I.bucket_off + 2 * k + 1, cnt, off, P);
+    const uint32_t o = node_off[i] + k;
+    if (comp == 0) {  // F = X_l + 2 X_r
+        xyzz_dbl(r, r);
+        xyzz_add(r, l);
+        store_vec(Fo + o, r);
+    } else {
+        xyzz_add(l, r);
+        if (comp == 2) xyzz_dbl(l, l);
+        store_vec((comp == 1 ? So : Do) + o, l);
+    }
+}
+
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_tree_level(const uint64_t* __restrict__ wp, int ninst,
+                                                       const uint32_t* __restrict__ node_off,
+                                                       const uint32_t* __restrict__ cnt_in,
+                                                       const Xyzz<F>* __restrict__ Fi, const Xyzz<F>* __restrict__ Si,
+                                                       const Xyzz<F>* __restrict__ Di, Xyzz<F>* __restrict__ Fo,
+                                                       Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t N = wp[ninst];
+    if (t >= 3 * N) return;
+    const uint32_t comp = (uint32_t)(t / N);
+    const uint64_t tn = t - comp * N;
+    const int i = find_slot(wp, ninst, tn);
+    const uint32_t k = (uint32_t)(tn - wp[i]);
+    const uint32_t base = node_off[i], n = cnt_in[i];
+    const bool has_r = 2 * k + 1 < n;
+    Xyzz<F> a, b;
+    if (comp == 0) {  // F_l + D_r + F_r
+        load_vec(a, Fi + base + 2 * k);
+        if (has_r) {
+            load_vec(b, Di + base + 2 * k + 1);
+            xyzz_add(a, b);
+            load_vec(b, Fi + base + 2 * k + 1);
+            xyzz_add(a, b);
+        }
+        store_vec(Fo + base + k, a);
+    } else if (comp == 1) {
+        load_vec(a, Si + base + 2 * k);
+        if (has_r) {
+            load_vec(b, Si + base + 2 * k + 1);
+            xyzz_add(a, b);
+        }
+        store_vec(So + base + k, a);
+    } else {
+        load_vec(a, Di + base + 2 * k);
+        if (has_r) {
+            load_vec(b, Di + base + 2 * k + 1);
+            xyzz_add(a, b);
+        }
+        xyzz_dbl(a, a);
+        store_vec(Do + base + k, a);
+    }
+}
+
+template <class F>
+__global__ void k_tree_out(int ninst, const uint32_t* __restrict__ node_off, const Xyzz<F>* __restrict__ Fi,
+                           Xyzz<F>* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < ninst) {
+        Xyzz<F> a;
+        load_vec(a, Fi + node_off[i]);
+        store_vec(out + i, a);
+    }
+}
+
+template <class F>
+static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>* pts, const Fr* scalars,
+                      void* out_dev, hipStream_t s) {
+    if (ninst <= 0) return;
+    MsmSorted so = msm_sort(ws, ih, ninst, scalars, s);
+    const bool g2 = sizeof(F) == sizeof(Fq2);
+    const uint32_t nb = so.nb;
+    const uint64_t tot_refs = so.tot_refs;
+    // level 1: affine references -> XYZZ partials, one per segment of kSeg references
+    const size_t psz = sizeof(Xyzz<F>);
+    const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
+    auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
+    auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
+    launch_seg_counts(so.counts, nb, so.segcnt, kSeg1, s);
+    exclusive_scan(ws, so.segcnt, so.soa, nb + 1, s);
+    kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
+    hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((max_segs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.soa,
+                       nb, so.offs, so.counts, so.refs, pts, PA);
+    // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
+    kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s);
+    uint32_t* cur_cnt = so.segcnt;
+    uint32_t* cur_off = so.soa;
+    uint32_t* nxt_off = so.sob;
+    uint32_t* spare_cnt = so.spare;
+    Xyzz<F>* cur = PA;
+    Xyzz<F>* nxt = PB;
+    uint64_t cur_max_segs = max_segs;
+    uint32_t m = (so.maxc + kSeg1 - 1) / kSeg1;
+    while (m > 1) {
+        launch_seg_counts(cur_cnt, nb, spare_cnt, kSeg, s);
+        exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
+        uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
+        kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
+        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3((unsigned)((nsegs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
+                           nxt_off, nb, cur_off, cur_cnt, cur, nxt);
+        kp_end((double)(cur_max_segs + nsegs) * psz, s);
+        std::swap(cur, nxt);
+        std::swap(cur_off, nxt_off);
+        std::swap(cur_cnt, spare_cnt);
+        cur_max_segs = nsegs;
+        m = (m + kSeg - 1) / kSeg;
+    }
+    // bucket weighting tree
+    std::vector<uint32_t> node_off(ninst), cnt(ninst);
+    uint32_t tot_nodes = 0;
+    int levels = 0;
+    for (int i = 0; i < ninst; ++i) {
+        node_off[i] = tot_nodes;
+        cnt[i] = 1u << (so.insts[i].c - 2);  // nodes after the leaf level (B / 2; c >= 3)
+        tot_nodes += cnt[i];
+        levels = std::max(levels, (int)so.insts[i].c - 2);
+    }
+    // per-level work prefixes: 3 threads per output node; per-level input node counts
+    std::vector<uint64_t> wp((size_t)(levels + 1) * (ninst + 1));
+    std::vector<uint32_t> cin((size_t)(levels + 1) * ninst);
+    for (int lv = 0; lv <= levels; ++lv) {
+        uint64_t acc = 0;
+        for (int i = 0; i < ninst; ++i) {
+            uint32_t nin = lv == 0 ? (cnt[i] * 2) : std::max(1u, cnt[i] >> (lv - 1));
+            uint32_t nout = lv == 0 ? cnt[i] : std::max(1u, cnt[i] >> lv);
+            cin[(size_t)lv * ninst + i] = nin;
+            wp[(size_t)lv * (ninst + 1) + i] = acc;
+            acc += nout;
+        }
+        wp[(size_t)lv * (ninst + 1) + ninst] = acc;
+    }
+    const size_t tbytes = 8 * wp.size() + 4 * cin.size() + 4 * node_off.size();
+    auto* tp = (uint8_t*)ws->tprefix.ensure(tbytes);
+    uint64_t* d_wp = (uint64_t*)tp;
+    uint32_t* d_cin = (uint32_t*)(tp + 8 * wp.size());
+    uint32_t* d_noff = d_cin + cin.size();
+    HIPCHK(hipMemcpyAsync(d_wp, wp.data(), 8 * wp.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_cin, cin.data(), 4 * cin.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_noff, node_off.data(), 4 * node_off.size(), hipMemcpyHostToDevice, s));
+    auto* TA = (Xyzz<F>*)ws->tree_a.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
+    auto* TB = (Xyzz<F>*)ws->tree_b.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
+    Xyzz<F>* A3[3] = {TA, TA + tot_nodes, TA + 2 * (size_t)tot_nodes};
+    Xyzz<F>* B3[3] = {TB, TB + tot_nodes, TB + 2 * (size_t)tot_nodes};
+    kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
+    {
+        uint64_t work = 3 * wp[ninst];
+        hipLaunchKernelGGL(k_tree_leaf<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
+                           so.d_insts, d_wp, ninst, d_noff, cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
+    }
+    for (int lv = 1; lv <= levels; ++lv) {
+        uint64_t work = 3 * wp[(size_t)lv * (ninst + 1) + ninst];
+        hipLaunchKernelGGL(k_tree_level<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
+                           d_wp + (size_t)lv * (ninst + 1), ninst, d_noff, d_cin + (size_t)lv * ninst, A3[0], A3[1],
+                           A3[2], B3[0], B3[1], B3[2]);
+        std::swap(A3, B3);
+    }
+    hipLaunchKernelGGL(k_tree_out<F>, dim3((ninst + 63) / 64), dim3(64), 0, s, ninst, d_noff, A3[0], (Xyzz<F>*)out_dev);
+    kp_end((double)nb * psz, s);
+    HIPCHK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ PP preprocessing
+template <class F>
+DEV void xyzz_from_aff(Xyzz<F>& r, const Aff<F>& a) {
+    if (aff_is_sentinel(a)) {
+        xyzz_set_inf(r);
+        return;
+    }
+    r.x = a.x;
+    r.y = a.y;
+    FieldOps<F>::one(r.zz);
+    FieldOps<F>::one(r.zzz);
+}
+
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_precompute(const Aff<F>* __restrict__ raw, uint64_t count, int pair_sum,
+                                                       int c, int W, Xyzz<F>* __restrict__ tmp) {
+    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    Xyzz<F> P;
+    if (pair_sum) {
+        Aff<F> a, b;
+        load_vec(a, raw + 2 * j);
+        load_vec(b, raw + 2 * j + 1);
+        xyzz_from_aff(P, a);
+        if (!aff_is_sentinel(b)) xyzz_madd(P, b, false);
+    } else {
+        Aff<F> a;
+        load_vec(a, raw + j);
+        xyzz_from_aff(P, a);
+    }
+    for (int w = 0; w < W; ++w) {
+        store_vec(tmp + (uint64_t)w * count + j, P);
+        if (w + 1 < W)
+            for (int k = 0; k < c; ++k) xyzz_dbl(P, P);
+    }
+}
+
+// XYZZ -> affine with Montgomery's batch-inversion trick over chunks of kNormChunk points
+static constexpr int kNormChunk = 32;
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_normalize(const Xyzz<F>* __restrict__ in, uint64_t n, Aff<F>* __restrict__ out) {
+    using O = FieldOps<F>;
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t b = t * kNormChunk;
+    if (b >= n) return;
+    const uint64_t e = min(b + (uint64_t)kNormChunk, n);
+    F acc;
+    O::one(acc);
+    for (uint64_t k = b; k < e; ++k) {
+        Xyzz<F> p;
+        load_vec(p, in + k);
+        out[k].x = acc;  // prefix product parked in the output
+        if (!xyzz_is_inf(p)) {
+            F d;
+            O::mul(d, p.zz, p.zzz);
+            O::mul(acc, acc, d);
+        }
+    }
+    F inv;
+    O::inv(inv, acc);
+    for (uint64_t k = e; k-- > b;) {
+        Xyzz<F> p;
+        load_vec(p, in + k);
+        if (xyzz_is_inf(p)) {
+            Aff<F> a;
+            aff_set_sentinel(a);
+            store_vec(out + k, a);
+            continue;
+        }
+        F d, di, izz, izzz;
+        O::mul(di, inv, out[k].x);
+        O::mul(d, p.zz, p.zzz);
+        O::mul(inv, inv, d);
+        O::mul(izz, di, p.zzz);
+        O::mul(izzz, di, p.zz);
+        Aff<F> a;
+        O::mul(a.x, p.x, izz);
+        O::mul(a.y, p.y, izzz);
+        store_vec(out + k, a);
+    }
+}
+
+template <class F>
+static void precompute_windows_t(const Aff<F>* raw, uint64_t count, bool pair_sum, int c, int W, Aff<F>* dst, void* tmp,
+                               hipStream_t s) {
+    if (!count) return;
+    Xyzz<F>* t = (Xyzz<F>*)tmp;
+    hipLaunchKernelGGL(k_precompute<F>, dim3((unsigned)((count + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, raw, count,
+                       pair_sum ? 1 : 0, c, W, t);
+    const uint64_t n = count * (uint64_t)W;
+    const uint64_t nt = (n + kNormChunk - 1) / kNormChunk;
+    hipLaunchKernelGGL(k_normalize<F>, dim3((unsigned)((nt + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, t, n, dst);
+    HIPCHK(hipGetLastError());
+}
+// ------------------------------------------------------------------ fixed-base (keygen)
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_fixed_base(const Aff<F>* __restrict__ table, const Fr* __restrict__ scalars,
+                                                       uint64_t n, Xyzz<F>* __restrict__ tmp) {
+    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    Fr m, s;
+    load_vec(m, scalars + j);
+    fe_from_mont(s, m);
+    Xyzz<F> acc;
+    xyzz_set_inf(acc);
+    for (int w = 0; w < 32; ++w) {
+        const uint32_t d = (s.v[w >> 2] >> (8 * (w & 3))) & 0xffu;
+        if (d) {
+            Aff<F> a;
+            load_vec(a, table + w * 256 + d);
+            xyzz_madd(acc, a, false);
+        }
+    }
+    store_vec(tmp + j, acc);
+}
+template <class F>
+static void fixed_base_t(const Aff<F>* table, const Fr* scalars, uint64_t n, Aff<F>* out, void* tmp, hipStream_t s) {
+    if (!n) return;
+    Xyzz<F>* t = (Xyzz<F>*)tmp;
+    hipLaunchKernelGGL(k_fixed_base<F>, dim3((unsigned)((n + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, table, scalars,
+                       n, t);
+    const uint64_t nt = (n + kNormChunk - 1) / kNormChunk;
+    hipLaunchKernelGGL(k_normalize<F>, dim3((unsigned)((nt + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, t, n, out);
+    HIPCHK(hipGetLastError());
+}
+}  // namespace spx

@@ -1,15 +1,24 @@
 #!/usr/bin/env python
 """bench.py — R1CS constraints proved per second (BASELINE.json metric) on N MI355X.
 
-One step = one complete `MLArgumentForR1CS::prove` (/root/reference/src/lib.rs:58-146) of a
+One proof = one complete `MLArgumentForR1CS::prove` (/root/reference/src/lib.rs:58-146) of a
 synthetic uniform-3n R1CS instance (2^20 constraints, |v| = 32, nnz = 3n) with the
-witness already resident in HBM: Fiat-Shamir transcript (including absorbing A, B, C), G1 commit
-MSM, two mKZG openings (G2 MSMs), SpMVs, eq tables, both sumchecks, proof serialization. Setup
-(keygen), index and witness upload are outside the timed region, as in benchmark.rs:26-35.
+witness already resident in HBM: Fiat-Shamir transcript (including absorbing A, B, C on every
+proof), G1 commit MSM, two mKZG openings (G2 MSMs), SpMVs, eq tables, both sumchecks, proof
+serialization. Setup (keygen), index and witness upload are outside the timed region, as in
+benchmark.rs:26-35.
 
-N > 1: one process per GPU (torch.distributed.run); the proof is sharded over the ranks
-(hypercube blocks, RCCL AllGather of per-round partials), so `value` = n / wall time of one
-sharded proof ("scaling": "strong": total work fixed).
+One step = a batch of --inflight proofs; the K timed steps run as one continuous pipeline of K x B
+proofs through spx_prove_many (B host worker threads, each with its own HIP stream and MSM
+workspace, each proving its share back to back), so the sequential host Blake2s absorption of the
+matrices (~150 MB per proof) overlaps other proofs' GPU work instead of idling the GPU.
+value = constraints proved per second over the timed region (whole job). The single-proof latency
+and the index-cached-transcript variant are reported beside it.
+
+N > 1: one process per GPU (torch.distributed.run); every proof is sharded over the ranks
+(hypercube blocks; per-round partials exchanged by an on-node shared-memory allgather, one
+communicator per proof in flight; --comm rccl uses RCCL AllGather instead), so "scaling" is
+"strong" (total work per step fixed).
 
 Output: ONE JSON line on rank 0 (metric, value, roofline of the dominant kernel measured live with
 HIP events on the library's stream, cpu_baseline from the test oracle on a bounded sample).
@@ -24,6 +33,26 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# HIP kernel (short rocprofv3 name) behind each kernel-stats id
+KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
+        "open_level": "k_open_level", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq>",
+        "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq>", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(kname):
+    """HBM bytes per launch of `kname` from the committed rocprofv3 PMC passes (tools/pmc_summary.py)."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    sym = KSYM.get(kname)
+    rec = d.get("kernels", {}).get(sym) if sym else None
+    if not rec or rec.get("traffic_bytes") is None:
+        return None
+    return rec["traffic_bytes"]
+
 
 KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
           "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]
@@ -111,6 +140,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
+                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather")
+    ap.add_argument("--inflight", type=int, default=8, help="proofs in flight (worker contexts) = proofs per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,11 +155,21 @@ def main():
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 
     spx = load_product()
-    ctx = spx.Context(local)
-    if world > 1:
-        uid = [spx.comm_unique_id() if rank == 0 else None]
+    B = max(1, args.inflight)
+    # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
+    device = 0 if os.environ.get("SPX_BENCH_SAME_GPU") == "1" else local
+    ctxs = [spx.Context(device) for _ in range(B)]
+    ctx = ctxs[0]
+    if world > 1 and args.comm == "rccl":
+        uid = [[spx.comm_unique_id() for _ in range(B)] if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx.set_comm_rccl(uid[0], rank, world)
+        for k, c in enumerate(ctxs):
+            c.set_comm_rccl(uid[0][k], rank, world)
+    elif world > 1:
+        name = [spx.shm_name() if rank == 0 else None]
+        dist.broadcast_object_list(name, src=0)
+        for k, c in enumerate(ctxs):
+            c.set_comm_shm("%s_%d" % (name[0], k), rank, world)
 
     log_n, log_v = args.log_n, args.log_v
     n = 1 << log_n
@@ -150,44 +192,55 @@ def main():
     def prove(cached=False):
         return spx.MLArgumentForR1CS.prove_witness(pk, wit, pp, mode=args.mode, seed=7, cached=cached)
 
-    proof = None
-    for _ in range(args.warmup):
-        proof = prove()
+    def prove_batch(steps, cached=False):
+        return spx.MLArgumentForR1CS.prove_many(ctxs, pk, [wit] * (B * steps), pp, mode=args.mode, seed=7, cached=cached)
+
+    def timed(fn):
+        barrier()
+        t0 = time.perf_counter()
+        r = fn()
+        barrier()
+        return r, time.perf_counter() - t0
+
+    proofs = prove_batch(max(1, args.warmup))
     L = spx.lib()
     if not args.no_stats:
         spx._check(L.spx_kernel_stats_enable(ctx.h, 1))
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        proof = prove()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    phases = ctx.last_timings()
+    # ---- timed region (headline): K steps x B full proofs, pipelined over B workers
+    proofs, elapsed = timed(lambda: prove_batch(args.steps))
     stats = {}
     if not args.no_stats:
         for k, name in enumerate(KNAMES):
-            cnt, ms, by = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
-            spx._check(L.spx_kernel_stats(ctx.h, k, ctypes.byref(cnt), ctypes.byref(ms), ctypes.byref(by)))
+            cnt, kms, by = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+            spx._check(L.spx_kernel_stats(ctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
             if cnt.value:
-                stats[name] = {"launches": cnt.value / args.steps, "ms": ms.value / args.steps, "bytes": by.value / args.steps}
+                # ctx 0 proves one proof per step
+                stats[name] = {"launches": cnt.value / args.steps, "ms": kms.value / args.steps, "bytes": by.value / args.steps}
         spx._check(L.spx_kernel_stats_enable(ctx.h, 0))
-    # index-cached transcript variant (matrix absorption moved to index time; bit-identical proof)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        p2 = prove(cached=True)
-    barrier()
-    elapsed_cached = time.perf_counter() - t0
-    assert p2 == proof, "cached-transcript proof differs"
+    assert all(p == proofs[0] for p in proofs), "concurrent proofs differ"
+    proof = proofs[0]
+    # ---- single-proof latency (one proof at a time) and its phase split
+    def single():
+        for _ in range(args.steps):
+            r = prove()
+        return r
 
-    ms = elapsed / args.steps * 1e3
+    p1, elapsed_single = timed(single)
+    assert p1 == proof, "single proof differs from the batched one"
+    phases = ctx.last_timings()
+    # ---- index-cached transcript variant (matrix absorption moved to index time; bit-identical)
+    p2, elapsed_cached = timed(lambda: prove_batch(args.steps, cached=True))
+    assert all(p == proof for p in p2), "cached-transcript proof differs"
+
+    ms = elapsed / args.steps * 1e3  # per step (B proofs)
     ms_c = elapsed_cached / args.steps * 1e3
+    ms_1 = elapsed_single / args.steps * 1e3
     if dist is not None:
         import torch
 
-        t = torch.tensor([ms, ms_c], dtype=torch.float64)
+        t = torch.tensor([ms, ms_c, ms_1], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, ms_c = float(t[0]), float(t[1])
+        ms, ms_c, ms_1 = float(t[0]), float(t[1]), float(t[2])
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -207,7 +260,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(dom),
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
             "bytes_per_launch": per_launch,
             "avg_launch_us": round(avg_s * 1e6, 2),
             "note": "algorithmic bytes / live HIP-event duration; MSM bucket accumulation is integer-VALU bound (see DESIGN.md)",
@@ -217,7 +271,7 @@ def main():
         cpu = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds)
     out = {
         "metric": "R1CS constraints proved/sec at 2^%d" % log_n,
-        "value": round(n / (ms / 1e3), 1),
+        "value": round(B * n / (ms / 1e3), 1),
         "unit": "constraints/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -229,15 +283,20 @@ def main():
         "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
         "data": "synthetic",
         "config": {
-            "workload": "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, full prove + commit + 2 openings, %s transcript"
-            % ("uniform-3n" if args.kind == 0 else "ref-shaped", log_n, 1 << log_v, nnz, args.mode.upper()),
+            "workload": "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, full prove + commit + 2 openings, %s transcript, "
+            "%d proofs in flight per step" % ("uniform-3n" if args.kind == 0 else "ref-shaped", log_n, 1 << log_v, nnz,
+                                              args.mode.upper(), B),
             "log_n": log_n,
+            "proofs_per_step": B,
             "parallelism": "shard%d" % world,
+            "comm": args.comm if world > 1 else None,
         },
-        "value_index_cached_transcript": round(n / (ms_c / 1e3), 1),
+        "ms_per_proof_single": round(ms_1, 3),
+        "value_single_proof": round(n / (ms_1 / 1e3), 1),
+        "value_index_cached_transcript": round(B * n / (ms_c / 1e3), 1),
         "ms_per_step_index_cached_transcript": round(ms_c, 3),
         "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
-        "kernels_ms_per_step": {k: round(v["ms"], 3) for k, v in stats.items()},
+        "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in stats.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
         "setup_s": round(t_setup, 2),

@@ -72,6 +72,15 @@ int spx_ctx_destroy(spx_ctx *ctx);
  * (e.g. torch.distributed), then every rank calls spx_ctx_set_comm_rccl. */
 int spx_comm_unique_id(uint8_t id_out[128]);
 int spx_ctx_set_comm_rccl(spx_ctx *ctx, const uint8_t id[128], int rank, int world);
+/* On-node shared-memory communicator (default for one process per GPU on one host): every rank
+ * passes the same `name` (rank 0 makes it unique, e.g. "spx_<random hex>_<k>", and distributes it
+ * out of band), one name per context. The exchanges of a sharded proof are host-side and tiny, so
+ * no GPU queue is involved (multi-GPU). The standalone form is a host-only
+ * allgather (tests, other transports' validation). */
+int spx_ctx_set_comm_shm(spx_ctx *ctx, const char *name, int rank, int world);
+int spx_comm_shm_create(const char *name, int rank, int world, void **comm_out);
+int spx_comm_shm_allgather(void *comm, const void *send, void *recv, size_t bytes);
+int spx_comm_shm_destroy(void *comm);
 /* In-process test communicator: `world` contexts sharing one exchange object (shards of one proof
  * driven by `world` host threads). group_create returns a handle; each ctx joins with its rank. */
 int spx_comm_group_create(int world, void **group_out);
@@ -96,6 +105,14 @@ int spx_prove(spx_ctx *ctx, spx_pk *idx, const uint8_t *v, size_t nv, const uint
 /* witness already resident in HBM (the benchmarked form) */
 int spx_prove_witness(spx_ctx *ctx, spx_pk *idx, spx_witness *wit, spx_pp *pp, const spx_prove_opts *opts,
                       uint8_t *out, size_t cap, size_t *len);
+/* Proves nproofs witnesses of one index concurrently: worker k drives ctxs[k] (its own HIP stream,
+ * MSM workspace and communicator) and proves witnesses k, k + nctx, ... in order. Every proof does
+ * the complete per-proof work of spx_prove_witness (transcript absorption of A, B, C included unless
+ * opts->cached_matrix_transcript). Proof i is written to out + i * stride, its length to lens[i].
+ * All contexts must be on the device (and communicator rank) the index was built for. Throughput
+ * form of lib.rs:58-146 for a prover serving many witnesses; returns the first failure's status. */
+int spx_prove_many(spx_ctx **ctxs, int nctx, spx_pk *idx, spx_witness **wits, int nproofs, spx_pp *pp,
+                   const spx_prove_opts *opts, uint8_t *out, size_t stride, size_t *lens);
 /* per-phase device timings of the last prove on this ctx, microseconds */
 int spx_last_timings(spx_ctx *ctx, double *out, int cap, int *n);
 

@@ -74,6 +74,10 @@ EXPORTED = [
     "spx_ctx_destroy",
     "spx_comm_unique_id",
     "spx_ctx_set_comm_rccl",
+    "spx_ctx_set_comm_shm",
+    "spx_comm_shm_create",
+    "spx_comm_shm_allgather",
+    "spx_comm_shm_destroy",
     "spx_comm_group_create",
     "spx_comm_group_destroy",
     "spx_ctx_set_comm_group",
@@ -88,6 +92,7 @@ EXPORTED = [
     "spx_proof_size",
     "spx_prove",
     "spx_prove_witness",
+    "spx_prove_many",
     "spx_last_timings",
     "spx_sum_over_y",
     "spx_eval_on_x",
@@ -117,6 +122,10 @@ def lib():
     L.spx_ctx_destroy.argtypes = [vp]
     L.spx_comm_unique_id.argtypes = [ctypes.c_void_p]
     L.spx_ctx_set_comm_rccl.argtypes = [vp, u8p, ctypes.c_int, ctypes.c_int]
+    L.spx_ctx_set_comm_shm.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    L.spx_comm_shm_create.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_comm_shm_allgather.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, sz]
+    L.spx_comm_shm_destroy.argtypes = [vp]
     L.spx_comm_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
@@ -132,6 +141,8 @@ def lib():
     L.spx_proof_size.argtypes = [ctypes.c_int, ctypes.c_int]
     L.spx_prove.argtypes = [vp, vp, u8p, sz, u8p, sz, vp, ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_prove_witness.argtypes = [vp, vp, vp, vp, ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_prove_many.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, ctypes.POINTER(vp), ctypes.c_int, vp,
+                                 ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.spx_sum_over_y.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
     L.spx_eval_on_x.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
@@ -220,6 +231,10 @@ class Context:
     def set_comm_rccl(self, unique_id, rank, world):
         _check(lib().spx_ctx_set_comm_rccl(self.h, bytes(unique_id), int(rank), int(world)))
 
+    def set_comm_shm(self, name, rank, world):
+        """On-node shared-memory communicator; every rank passes the same name (one per context)."""
+        _check(lib().spx_ctx_set_comm_shm(self.h, name.encode(), int(rank), int(world)))
+
     def set_comm_group(self, group, rank):
         _check(lib().spx_ctx_set_comm_group(self.h, group.h, int(rank)))
 
@@ -245,6 +260,37 @@ class CommGroup:
                 lib().spx_comm_group_destroy(self.h)
         except Exception:
             pass
+
+
+class ShmComm:
+    """Standalone host allgather over the shared-memory transport (no GPU needed)."""
+
+    def __init__(self, name, rank, world):
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_shm_create(name.encode(), int(rank), int(world), ctypes.byref(h)))
+        self.h, self.world = h, int(world)
+
+    def allgather(self, data):
+        data = bytes(data)
+        out = ctypes.create_string_buffer(len(data) * self.world)
+        _check(lib().spx_comm_shm_allgather(self.h, data, out, len(data)))
+        return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(self.world)]
+
+    def close(self):
+        if self.h:
+            lib().spx_comm_shm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shm_name():
+    """A fresh segment name (rank 0 draws it and distributes it)."""
+    return "spx_%016x" % int.from_bytes(os.urandom(8), "little")
 
 
 def comm_unique_id():
@@ -352,6 +398,21 @@ class MLArgumentForR1CS:
         o = _opts(mode, seed, cached)
         _check(lib().spx_prove_witness(pk.ctx.h, pk.h, wit.h, pp.h, ctypes.byref(o), out, cap, ctypes.byref(n)))
         return out.raw[: n.value]
+
+
+    @staticmethod
+    def prove_many(ctxs, pk, wits, pp, mode="fs", seed=0, cached=False):
+        """Proves every witness in `wits` concurrently, one worker per context (spx_prove_many)."""
+        cap = lib().spx_proof_size(pk.log_n, 0)
+        n = len(wits)
+        out = ctypes.create_string_buffer(cap * max(n, 1))
+        lens = (ctypes.c_size_t * max(n, 1))()
+        ch = (ctypes.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+        wh = (ctypes.c_void_p * max(n, 1))(*[w.h for w in wits])
+        o = _opts(mode, seed, cached)
+        _check(lib().spx_prove_many(ch, len(ctxs), pk.h, wh, n, pp.h, ctypes.byref(o), out, cap, lens))
+        raw = out.raw
+        return [raw[i * cap : i * cap + lens[i]] for i in range(n)]
 
 
 class MatrixExtension:

@@ -3,8 +3,11 @@
 // todo!(), /root/reference/src/error.rs:23-27).
 #include "../../include/spartan_hip.h"
 
+#include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "prover.hpp"
 
@@ -112,6 +115,27 @@ int spx_ctx_set_comm_rccl(spx_ctx* ctx, const uint8_t id[128], int rank, int wor
         ctx->c->comm = spx::make_rccl_comm(id, rank, world, ctx->c->device, ctx->c->stream);
     });
 }
+int spx_ctx_set_comm_shm(spx_ctx* ctx, const char* name, int rank, int world) {
+    return guard([&] {
+        if (!ctx) spx::invalid("null context");
+        ctx->c->comm = spx::make_shm_comm(name, rank, world);
+    });
+}
+int spx_comm_shm_create(const char* name, int rank, int world, void** comm_out) {
+    return guard([&] {
+        if (!comm_out) spx::invalid("null output");
+        *comm_out = spx::make_shm_comm(name, rank, world).release();
+    });
+}
+int spx_comm_shm_allgather(void* comm, const void* send, void* recv, size_t bytes) {
+    return guard([&] {
+        if (!comm || (bytes && (!send || !recv))) spx::invalid("null argument");
+        static_cast<spx::Comm*>(comm)->allgather(send, recv, bytes);
+    });
+}
+int spx_comm_shm_destroy(void* comm) {
+    return guard([&] { delete static_cast<spx::Comm*>(comm); });
+}
 int spx_comm_group_create(int world, void** group_out) {
     return guard([&] {
         if (world < 1) spx::invalid("bad world");
@@ -197,6 +221,54 @@ int spx_prove_witness(spx_ctx* ctx, spx_pk* idx, spx_witness* wit, spx_pp* pp, c
         set_dev(ctx);
         copy_out(spx::prove(*ctx->c, *idx->i, *wit->w, *pp->p, opts_of(opts)), out, cap, len);
     });
+}
+int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, int nproofs, spx_pp* pp,
+                   const spx_prove_opts* opts, uint8_t* out, size_t stride, size_t* lens) {
+    if (!ctxs || nctx < 1 || !idx || !wits || nproofs < 0 || !pp || !out || !lens) {
+        g_err = "spx_prove_many: bad arguments";
+        return SPX_INVALID_ARGUMENT;
+    }
+    for (int k = 0; k < nctx; ++k)
+        if (!ctxs[k]) {
+            g_err = "spx_prove_many: null context";
+            return SPX_INVALID_ARGUMENT;
+        }
+    for (int i = 0; i < nproofs; ++i)
+        if (!wits[i]) {
+            g_err = "spx_prove_many: null witness";
+            return SPX_INVALID_ARGUMENT;
+        }
+    const spx::ProveOpts o = opts_of(opts);
+    std::vector<int> st(nctx, SPX_OK);
+    std::vector<std::string> msg(nctx);
+    auto work = [&](int k) {
+        for (int i = k; i < nproofs; i += nctx) {
+            int rc = guard([&] {
+                set_dev(ctxs[k]);
+                auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, *pp->p, o);
+                if (p.size() > stride) spx::invalid("proof buffer too small");
+                memcpy(out + (size_t)i * stride, p.data(), p.size());
+                lens[i] = p.size();
+            });
+            if (rc != SPX_OK) {
+                st[k] = rc;
+                msg[k] = g_err;
+                return;
+            }
+        }
+    };
+    const int nw = std::min(nctx, std::max(nproofs, 1));
+    std::vector<std::thread> th;
+    for (int k = 1; k < nw; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto& t : th) t.join();
+    for (int k = 0; k < nw; ++k)
+        if (st[k] != SPX_OK) {
+            g_err = msg[k];
+            return st[k];
+        }
+    g_err.clear();
+    return SPX_OK;
 }
 int spx_last_timings(spx_ctx* ctx, double* out, int cap, int* n) {
     return guard([&] {

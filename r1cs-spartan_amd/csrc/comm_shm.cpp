@@ -1,0 +1,109 @@
+// On-node shared-memory communicator (one process per GPU, all ranks on one host).
+//
+// What a sharded proof exchanges is tiny and lives on the host (3 Fr per sumcheck round, a few
+// affine points per MSM), because the host derives every Fiat-Shamir challenge. A
+// host transport keeps those exchanges off the GPU queues entirely: with several proofs in flight
+// per rank (one communicator each), device collectives issued from independent worker threads can
+// reach a hardware queue (GPU_MAX_HW_QUEUES = 4) in different orders on different ranks and
+// deadlock; a host allgather cannot. Latency is a few microseconds.
+//
+// Segment: [seq[r] (one cache line per rank)][2 buffers x world x kSlot bytes]. allgather #n writes
+// this rank's slot of buffer n&1, publishes seq[r] = n (release) and waits for every seq >= n
+// (acquire). Buffer n&1 is rewritten only by call n+2, which every rank starts after finishing call
+// n+1, i.e. after it has read call n's data.
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <string>
+
+#include "../../include/spartan_hip.h"
+#include "prover.hpp"
+
+namespace spx {
+
+namespace {
+constexpr int kMaxRanks = 64;
+constexpr size_t kSlot = 1 << 16;
+constexpr size_t kHdr = 64 * kMaxRanks;
+}  // namespace
+
+struct ShmComm : Comm {
+    int r, w;
+    std::string name;
+    uint8_t* base = nullptr;
+    size_t len = 0;
+    uint64_t n = 0;
+    ShmComm(const std::string& nm, int rank, int world) : r(rank), w(world) {
+        if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) invalid("shm comm: bad rank/world");
+        name = "/" + nm;
+        if (nm.find('/') != std::string::npos) invalid("shm comm: name must not contain '/'");
+        len = kHdr + 2 * (size_t)world * kSlot;
+        int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd < 0) throw SpxError(kDevice, "shm_open failed for " + name);
+        if (ftruncate(fd, (off_t)len) != 0) {
+            close(fd);
+            throw SpxError(kDevice, "ftruncate failed for " + name);
+        }
+        void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) throw SpxError(kDevice, "mmap failed for " + name);
+        base = (uint8_t*)p;
+        // rendezvous: every rank has mapped the segment once this completes; then drop the name
+        std::vector<int> ranks(world);
+        allgather(&r, ranks.data(), sizeof(int));
+        for (int k = 0; k < world; ++k)
+            if (ranks[k] != k) throw SpxError(kDevice, "shm comm: rank mismatch (stale segment name?)");
+        if (r == 0) shm_unlink(name.c_str());
+    }
+    ~ShmComm() override {
+        if (base) munmap(base, len);
+    }
+    std::atomic<uint64_t>& seq(int k) { return *reinterpret_cast<std::atomic<uint64_t>*>(base + 64 * k); }
+    uint8_t* slot(uint64_t call, int k) { return base + kHdr + ((call & 1) * w + k) * kSlot; }
+    int rank() const override { return r; }
+    int size() const override { return w; }
+    void one(const uint8_t* send, uint8_t* recv, size_t bytes, size_t rstride) {
+        const uint64_t c = ++n;
+        memcpy(slot(c, r), send, bytes);
+        seq(r).store(c, std::memory_order_release);
+        auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < w; ++k) {
+            unsigned spins = 0;
+            while (seq(k).load(std::memory_order_acquire) < c) {
+                if (++spins < 4096) {
+                    __builtin_ia32_pause();
+                    continue;
+                }
+                sched_yield();
+                if ((spins & 0xffff) == 0 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
+                    throw SpxError(kDevice, "shm allgather: rank " + std::to_string(k) + " did not arrive in 600 s");
+            }
+        }
+        for (int k = 0; k < w; ++k) memcpy(recv + k * rstride, slot(c, k), bytes);
+    }
+    void allgather(const void* send, void* recv, size_t bytes) override {
+        // messages larger than a slot go in slot-sized rounds
+        const uint8_t* s = (const uint8_t*)send;
+        uint8_t* d = (uint8_t*)recv;
+        size_t done = 0;
+        do {
+            size_t b = std::min(kSlot, bytes - done);
+            one(s + done, d + done, b, bytes);
+            done += b;
+        } while (done < bytes);
+    }
+};
+
+std::unique_ptr<Comm> make_shm_comm(const char* name, int rank, int world) {
+    if (!name || !*name) invalid("shm comm: empty name");
+    return std::unique_ptr<Comm>(new ShmComm(name, rank, world));
+}
+
+}  // namespace spx

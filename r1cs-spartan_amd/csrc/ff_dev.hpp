@@ -253,10 +253,16 @@ DEV void fe_inv(Fe<C>& r, const Fe<C>& a) {
 }
 
 // ---------------------------------------------------------------- Fq2
-// G2 code calls the Fq multiplication out of line: a fully inlined G2 point addition is ~30
-// inlined 12-limb Montgomery products (~30k instructions), which overflows the instruction
-// cache and takes minutes to compile per kernel. Arguments/results pass by value (VGPRs).
-#ifndef SPX_FQ2_INLINE_MUL
+// G2 code calls Fq2 products out of line: a fully inlined G2 point addition is ~30 inlined 12-limb
+// Montgomery products (~25k instructions), which overflows the instruction cache. SPX_F2_MODE:
+//   0: each Fq product is a call (smallest code, no ILP across the Karatsuba products)
+//   1: each Fq2 product / square is a call; its 3 (2) Fq products are inline and independent,
+//      so one wave overlaps their multiply-accumulate chains (G2 kernels run at occupancy 1)
+//   2: everything inline
+#ifndef SPX_F2_MODE
+#define SPX_F2_MODE 1
+#endif
+#if SPX_F2_MODE == 0
 static __device__ __noinline__ Fq fq_mul_call(Fq a, Fq b) {
     Fq r;
     fe_mul(r, a, b);
@@ -289,7 +295,7 @@ DEV void f2_neg(Fq2& r, const Fq2& a) {
     fe_neg(r.c1, a.c1);
 }
 DEV void f2_dbl(Fq2& r, const Fq2& a) { f2_add(r, a, a); }
-DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) {
+DEV void f2_mul_inl(Fq2& r, const Fq2& a, const Fq2& b) {
     Fq t0, t1, s0, s1, m;
     SPX_FQMUL(t0, a.c0, b.c0);
     SPX_FQMUL(t1, a.c1, b.c1);
@@ -300,7 +306,7 @@ DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) {
     fe_sub(m, m, t0);
     fe_sub(r.c1, m, t1);
 }
-DEV void f2_sqr(Fq2& r, const Fq2& a) {
+DEV void f2_sqr_inl(Fq2& r, const Fq2& a) {
     Fq s, d, p;
     fe_add(s, a.c0, a.c1);
     fe_sub(d, a.c0, a.c1);
@@ -308,6 +314,23 @@ DEV void f2_sqr(Fq2& r, const Fq2& a) {
     SPX_FQMUL(r.c0, s, d);
     fe_add(r.c1, p, p);
 }
+#if SPX_F2_MODE == 1
+static __device__ __noinline__ Fq2 f2_mul_call(Fq2 a, Fq2 b) {
+    Fq2 r;
+    f2_mul_inl(r, a, b);
+    return r;
+}
+static __device__ __noinline__ Fq2 f2_sqr_call(Fq2 a) {
+    Fq2 r;
+    f2_sqr_inl(r, a);
+    return r;
+}
+DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) { r = f2_mul_call(a, b); }
+DEV void f2_sqr(Fq2& r, const Fq2& a) { r = f2_sqr_call(a); }
+#else
+DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) { f2_mul_inl(r, a, b); }
+DEV void f2_sqr(Fq2& r, const Fq2& a) { f2_sqr_inl(r, a); }
+#endif
 DEV void f2_inv(Fq2& r, const Fq2& a) {
     Fq t0, t1, n;
     fe_sqr(t0, a.c0);

@@ -8,6 +8,8 @@
 // the gathered G-entry tables. Every rank replays the same transcript, so no challenge broadcast.
 #include "prover.hpp"
 
+#include <type_traits>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -36,7 +38,7 @@ Ctx::~Ctx() {
 uint8_t* Ctx::pinned(size_t b) {
     if (b > pin_bytes) {
         if (pin) SPX_HIP(hipHostFree(pin));
-        size_t nb = std::max<size_t>(b, 1 << 16);
+        size_t nb = std::max<size_t>(b, 1 << 20);
         SPX_HIP(hipHostMalloc((void**)&pin, nb));
         pin_bytes = nb;
     }
@@ -562,10 +564,10 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
     inst.size = (uint32_t)nl;
     inst.c = (uint32_t)P.g1_c;
     inst.W = (uint32_t)P.g1_W;
-    DevMem out(4 * sizeof(Fq));
-    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out.p, C.stream);
+    void* out = C.buf(Ctx::kSlotCommit, 4 * sizeof(Fq));
+    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out, C.stream);
     uint8_t* h = C.pinned(4 * sizeof(Fq));
-    SPX_HIP(hipMemcpyAsync(h, out.p, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h, out, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
     C.sync();
     Affine<HFq> part = xyzz_bytes_to_affine<HFq>(h);
     if (G == 1) return part;
@@ -583,17 +585,18 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
     const int nloc = L - g;  // local levels
     OpenOut res;
     res.proofs.resize(L);
-    DevMem pt(32 * L), q(32 * std::max<uint64_t>(nl, 1)), ra(32 * std::max<uint64_t>(nl / 2, 1)),
-        rb(32 * std::max<uint64_t>(nl / 4, 1));
-    SPX_HIP(hipMemcpyAsync(pt.p, point.data(), 32 * L, hipMemcpyHostToDevice, C.stream));
+    Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
+    Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * std::max<uint64_t>(nl, 1));
+    Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
+                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
+    SPX_HIP(hipMemcpyAsync(pt, point.data(), 32 * L, hipMemcpyHostToDevice, C.stream));  // pageable: staged
     std::vector<MsmInst> insts(nloc);
     const Fr* rin = z_local;
-    Fr* bufs[2] = {ra.as<Fr>(), rb.as<Fr>()};
     uint64_t qoff = 0;
     for (int i = 0; i < nloc; ++i) {
         const uint64_t half = nl >> (i + 1);
         Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, q.as<Fr>() + qoff, pt.as<Fr>() + i, half, C.stream);
+        launch_open_level(rin, rout, q + qoff, pt + i, half, C.stream);
         MsmInst& I = insts[i];
         const uint64_t full = 1ull << (L - i - 1);
         I.pts_off = P.g2_off[i] + (uint64_t)rank * half;
@@ -605,11 +608,11 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
         qoff += half;
         rin = rout;
     }
-    DevMem out(4 * sizeof(Fq2) * std::max(nloc, 1));
-    msm_run_g2(C.msm, insts.data(), nloc, P.g2_pre.as<G2Aff>(), q.as<Fr>(), out.p, C.stream);
+    void* out = C.buf(Ctx::kSlotOpenOut, 4 * sizeof(Fq2) * std::max(nloc, 1));
+    msm_run_g2(C.msm, insts.data(), nloc, P.g2_pre.as<G2Aff>(), q, out, C.stream);
     const size_t xb = 4 * sizeof(Fq2);
     uint8_t* h = C.pinned(xb * nloc + 32);
-    SPX_HIP(hipMemcpyAsync(h, out.p, xb * nloc, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h, out, xb * nloc, hipMemcpyDeviceToHost, C.stream));
     SPX_HIP(hipMemcpyAsync(h + xb * nloc, rin, 32, hipMemcpyDeviceToHost, C.stream));
     C.sync();
     std::vector<Affine<HFq2>> part(nloc);
@@ -653,11 +656,12 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
         tinsts.push_back(I);
     }
     res.eval = rg[0];
-    DevMem qd(32 * qs.size()), out2(xb * tinsts.size());
-    SPX_HIP(hipMemcpyAsync(qd.p, qs.data(), 32 * qs.size(), hipMemcpyHostToDevice, C.stream));
-    msm_run_g2(C.msm, tinsts.data(), (int)tinsts.size(), P.g2_pre.as<G2Aff>(), qd.as<Fr>(), out2.p, C.stream);
+    Fr* qd = C.buf<Fr>(Ctx::kSlotTailQ, 32 * qs.size());
+    void* out2 = C.buf(Ctx::kSlotTailOut, xb * tinsts.size());
+    SPX_HIP(hipMemcpyAsync(qd, qs.data(), 32 * qs.size(), hipMemcpyHostToDevice, C.stream));  // pageable: staged
+    msm_run_g2(C.msm, tinsts.data(), (int)tinsts.size(), P.g2_pre.as<G2Aff>(), qd, out2, C.stream);
     uint8_t* h2 = C.pinned(xb * tinsts.size());
-    SPX_HIP(hipMemcpyAsync(h2, out2.p, xb * tinsts.size(), hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h2, out2, xb * tinsts.size(), hipMemcpyDeviceToHost, C.stream));
     C.sync();
     for (size_t k = 0; k < tinsts.size(); ++k) res.proofs[nloc + k] = xyzz_bytes_to_affine<HFq2>(h2 + xb * k);
     return res;
@@ -711,11 +715,24 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     if (P.nv != L) invalid("public parameter nv != log_n");
     const int log_v = ilog2(nvv);
     Transcript T(o.mode == 1, o.seed);
+    const uint64_t seq = C.prove_seq++;
     if (o.cached && I.has_cache)
         T.set_state(I.cache);
-    else {
+    else if (G == 1) {
         Blake2s h;
         for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        T.set_state(h);
+    } else {
+        // the (sequential, ~150 MB at 2^20) absorption of A, B, C is done once per proof, by one rank
+        // in turn; the others take its Blake2s state from the allgather (bit-identical transcript)
+        static_assert(std::is_trivially_copyable<Blake2s>::value, "Blake2s state is shipped as bytes");
+        const int owner = (int)(seq % (uint64_t)G);
+        Blake2s h;
+        if (rank == owner)
+            for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        std::vector<uint8_t> all(sizeof(Blake2s) * G);
+        comm.allgather(&h, all.data(), sizeof(Blake2s));
+        memcpy(&h, all.data() + sizeof(Blake2s) * owner, sizeof(Blake2s));
         T.set_state(h);
     }
     {

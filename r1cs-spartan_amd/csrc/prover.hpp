@@ -109,6 +109,7 @@ struct GroupComm : Comm {
         st->barrier();
     }
 };
+std::unique_ptr<Comm> make_shm_comm(const char* name, int rank, int world);
 std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int rank, int world, int device, hipStream_t s);
 
 // ---------------------------------------------------------------- context
@@ -120,10 +121,19 @@ struct Ctx {
     // pinned staging
     uint8_t* pin = nullptr;
     size_t pin_bytes = 0;
-    // per-prove scratch
+    // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
+    // on other contexts are in flight)
     DevMem scratch;
+    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotTailQ, kSlotTailOut, kSlots };
+    DevMem slot[kSlots];
+    template <class T = void>
+    T* buf(int id, size_t bytes) {
+        slot[id].ensure(bytes);
+        return static_cast<T*>(slot[id].p);
+    }
     std::vector<std::pair<std::string, double>> timings;
     KProf kprof;
+    uint64_t prove_seq = 0;  // proofs started on this context (identical on every rank of its communicator)
     Ctx(int dev);
     ~Ctx();
     uint8_t* pinned(size_t b);

@@ -107,3 +107,22 @@ def test_prove_bit_exact(spx, ctx, oc, kind, log_n, log_v, mode):
     if got != want:
         i = next(k for k in range(len(got)) if got[k] != want[k])
         pytest.fail("proof differs from oracle at byte %d of %d" % (i, len(got)))
+
+
+@pytest.mark.parametrize("cached", [False, True])
+def test_prove_many_concurrent(spx, ctx, oc, cached):
+    """spx_prove_many: several contexts (streams, MSM workspaces) proving concurrently from one index;
+    every proof bit-exact vs the oracle, with and without the index-cached matrix transcript."""
+    log_n, log_v = 10, 4
+    inst = oc.Instance(0, log_n, log_v, 4242)
+    ppc = oc.PP.keygen(log_n, 4343)
+    pp = spx.PublicParameter.load(ctx, ppc.serialize())
+    mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
+    pk = spx.MLArgumentForR1CS.index(ctx, *mats)
+    wit = spx.Witness(ctx, inst.v_bytes, inst.w_bytes)
+    ctxs = [ctx] + [spx.Context(0) for _ in range(2)]
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
+    got = spx.MLArgumentForR1CS.prove_many(ctxs, pk, [wit] * 7, pp, cached=cached)
+    assert len(got) == 7
+    for g in got:
+        assert g == want

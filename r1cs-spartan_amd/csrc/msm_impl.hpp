@@ -1,33 +1,40 @@
 // Curve-templated MSM kernels and drivers; instantiated once per curve (msm_g1.hip, msm_g2.hip)
 // so the heavy big-integer code of G1 and G2 compiles in parallel.
 #pragma once
+#include "curve29.hpp"
 #include "msm_common.hpp"
 
 namespace spx {
 
 // ------------------------------------------------------------------ accumulation levels
+// Accumulation and weighting run in the radix-2^29 domain (ff29.hpp / curve29.hpp): tables and
+// partials in memory hold R = 2^406 Montgomery values (< 2p), packed into the 12-word layout.
 template <class F>
 __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict__ segoff, uint32_t nb,
                                                       const uint32_t* __restrict__ off,
                                                       const uint32_t* __restrict__ cnt,
                                                       const uint32_t* __restrict__ refs,
                                                       const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out) {
+    using T = typename R29<F>::T;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= segoff[nb]) return;
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
     const uint32_t start = off[b] + k * kSeg1;
     const uint32_t end = min(start + kSeg1, off[b] + cnt[b]);
-    Xyzz<F> acc;
-    xyzz_set_inf(acc);
+    X29<T> acc;
+    x29_set_inf(acc);
     for (uint32_t e = start; e < end; ++e) {
         const uint32_t r = refs[e];
         Aff<F> p;
         load_vec(p, pts + (r & 0x7fffffffu));
         if (aff_is_sentinel(p)) continue;
-        xyzz_madd(acc, p, (r >> 31) != 0);
+        T px, py;
+        R29<F>::unpack(px, p.x);
+        R29<F>::unpack(py, p.y);
+        x29_madd(acc, px, py, (r >> 31) != 0);
     }
-    store_vec(out + s, acc);
+    st29<F>(out + s, acc);
 }
 
 template <class F>
@@ -35,20 +42,21 @@ __global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restric
                                                        const uint32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ cnt,
                                                        const Xyzz<F>* __restrict__ in, Xyzz<F>* __restrict__ out) {
+    using T = typename R29<F>::T;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= segoff[nb]) return;
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
     const uint32_t start = off[b] + k * kSeg;
     const uint32_t end = min(start + kSeg, off[b] + cnt[b]);
-    Xyzz<F> acc;
-    load_vec(acc, in + start);
+    X29<T> acc;
+    ld29<F>(acc, in + start);
     for (uint32_t e = start + 1; e < end; ++e) {
-        Xyzz<F> p;
-        load_vec(p, in + e);
-        xyzz_add(acc, p);
+        X29<T> p;
+        ld29<F>(p, in + e);
+        x29_add(acc, p);
     }
-    store_vec(out + s, acc);
+    st29<F>(out + s, acc);
 }
 
 // ------------------------------------------------------------------ bucket weighting: low-depth tree
@@ -62,11 +70,12 @@ __global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restric
 // A missing right child (instances with fewer buckets) is the point at infinity: F and S pass
 // through unchanged, so all instances of a batch run the same number of levels.
 template <class F>
-DEV void ld_bucket(Xyzz<F>& x, uint32_t b, const uint32_t* cnt, const uint32_t* off, const Xyzz<F>* P) {
+DEV void ld_bucket(X29<typename R29<F>::T>& x, uint32_t b, const uint32_t* cnt, const uint32_t* off,
+                   const Xyzz<F>* P) {
     if (cnt[b])
-        load_vec(x, P + off[b]);
+        ld29<F>(x, P + off[b]);
     else
-        xyzz_set_inf(x);
+        x29_set_inf(x);
 }
 
 template <class F>
@@ -83,18 +92,18 @@ __global__ __launch_bounds__(kHeavy) void k_tree_leaf(const MsmInst* __restrict_
     const int i = find_slot(wp, ninst, tn);
     const uint32_t k = (uint32_t)(tn - wp[i]);
     const MsmInst I = insts[i];
-    Xyzz<F> l, r;
+    X29<typename R29<F>::T> l, r;
     ld_bucket(l, I.bucket_off + 2 * k, cnt, off, P);
     ld_bucket(r, I.bucket_off + 2 * k + 1, cnt, off, P);
     const uint32_t o = node_off[i] + k;
     if (comp == 0) {  // F = X_l + 2 X_r
-        xyzz_dbl(r, r);
-        xyzz_add(r, l);
-        store_vec(Fo + o, r);
+        x29_dbl(r);
+        x29_add(r, l);
+        st29<F>(Fo + o, r);
     } else {
-        xyzz_add(l, r);
-        if (comp == 2) xyzz_dbl(l, l);
-        store_vec((comp == 1 ? So : Do) + o, l);
+        x29_add(l, r);
+        if (comp == 2) x29_dbl(l);
+        st29<F>((comp == 1 ? So : Do) + o, l);
     }
 }
 
@@ -114,42 +123,47 @@ __global__ __launch_bounds__(kHeavy) void k_tree_level(const uint64_t* __restric
     const uint32_t k = (uint32_t)(tn - wp[i]);
     const uint32_t base = node_off[i], n = cnt_in[i];
     const bool has_r = 2 * k + 1 < n;
-    Xyzz<F> a, b;
+    X29<typename R29<F>::T> a, b;
     if (comp == 0) {  // F_l + D_r + F_r
-        load_vec(a, Fi + base + 2 * k);
+        ld29<F>(a, Fi + base + 2 * k);
         if (has_r) {
-            load_vec(b, Di + base + 2 * k + 1);
-            xyzz_add(a, b);
-            load_vec(b, Fi + base + 2 * k + 1);
-            xyzz_add(a, b);
+            ld29<F>(b, Di + base + 2 * k + 1);
+            x29_add(a, b);
+            ld29<F>(b, Fi + base + 2 * k + 1);
+            x29_add(a, b);
         }
-        store_vec(Fo + base + k, a);
+        st29<F>(Fo + base + k, a);
     } else if (comp == 1) {
-        load_vec(a, Si + base + 2 * k);
+        ld29<F>(a, Si + base + 2 * k);
         if (has_r) {
-            load_vec(b, Si + base + 2 * k + 1);
-            xyzz_add(a, b);
+            ld29<F>(b, Si + base + 2 * k + 1);
+            x29_add(a, b);
         }
-        store_vec(So + base + k, a);
+        st29<F>(So + base + k, a);
     } else {
-        load_vec(a, Di + base + 2 * k);
+        ld29<F>(a, Di + base + 2 * k);
         if (has_r) {
-            load_vec(b, Di + base + 2 * k + 1);
-            xyzz_add(a, b);
+            ld29<F>(b, Di + base + 2 * k + 1);
+            x29_add(a, b);
         }
-        xyzz_dbl(a, a);
-        store_vec(Do + base + k, a);
+        x29_dbl(a);
+        st29<F>(Do + base + k, a);
     }
 }
 
 template <class F>
 __global__ void k_tree_out(int ninst, const uint32_t* __restrict__ node_off, const Xyzz<F>* __restrict__ Fi,
                            Xyzz<F>* __restrict__ out) {
+    using T = typename R29<F>::T;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < ninst) {
-        Xyzz<F> a;
-        load_vec(a, Fi + node_off[i]);
-        store_vec(out + i, a);
+    if (i < ninst) {  // back to the R = 2^384 Montgomery domain, canonical, for the host
+        X29<T> a, b;
+        ld29<F>(a, Fi + node_off[i]);
+        f29_map(b.x, a.x, Q29::TO_R1);
+        f29_map(b.y, a.y, Q29::TO_R1);
+        f29_map(b.zz, a.zz, Q29::TO_R1);
+        f29_map(b.zzz, a.zzz, Q29::TO_R1);
+        st29<F>(out + i, b);
     }
 }
 
@@ -331,6 +345,24 @@ __global__ __launch_bounds__(kHeavy) void k_normalize(const Xyzz<F>* __restrict_
     }
 }
 
+// affine table, R = 2^384 canonical -> R = 2^406 canonical (in place); the sentinel (0, 0) maps to itself
+template <class F>
+__global__ __launch_bounds__(kHeavy) void k_aff_to_r29(Aff<F>* __restrict__ a, uint64_t n) {
+    using T = typename R29<F>::T;
+    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    Aff<F> p;
+    load_vec(p, a + j);
+    T x, y, mx, my;
+    R29<F>::unpack(x, p.x);
+    R29<F>::unpack(y, p.y);
+    f29_map(mx, x, Q29::FROM_R1);
+    f29_map(my, y, Q29::FROM_R1);
+    R29<F>::pack(p.x, mx);
+    R29<F>::pack(p.y, my);
+    store_vec(a + j, p);
+}
+
 template <class F>
 static void precompute_windows_t(const Aff<F>* raw, uint64_t count, bool pair_sum, int c, int W, Aff<F>* dst, void* tmp,
                                hipStream_t s) {
@@ -341,6 +373,7 @@ static void precompute_windows_t(const Aff<F>* raw, uint64_t count, bool pair_su
     const uint64_t n = count * (uint64_t)W;
     const uint64_t nt = (n + kNormChunk - 1) / kNormChunk;
     hipLaunchKernelGGL(k_normalize<F>, dim3((unsigned)((nt + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, t, n, dst);
+    hipLaunchKernelGGL(k_aff_to_r29<F>, dim3((unsigned)((n + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, dst, n);
     HIPCHK(hipGetLastError());
 }
 // ------------------------------------------------------------------ fixed-base (keygen)

@@ -142,7 +142,7 @@ def main():
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
                     help="N > 1 transport: on-node shared memory (default) or RCCL AllGather")
-    ap.add_argument("--inflight", type=int, default=8, help="proofs in flight (worker contexts) = proofs per step")
+    ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts) = proofs per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -611,15 +611,23 @@ def prove(pk, v, w, pp, fs=None, trace=None):
 
 
 # ----------------------------------------------------------------------------- verifier
-def verify(vk, v, proof, vp, fs=None):
-    """lib.rs:147-212 with verifier.rs:143-512. Raises on rejection, returns True on accept."""
+def verify(vk, v, proof, vp, fs=None, feed_matrices=None, eval_rr=None, check_pairings=True, out=None):
+    """lib.rs:147-212 with verifier.rs:143-512. Raises on rejection, returns True on accept.
+
+    Hooks for full-size tests (same checks, faster plumbing): `feed_matrices(fs)` absorbs A, B, C
+    (default: matrix_bytes of vk's row lists); `eval_rr(r_x, r_y)` returns (A, B, C)(r_x, r_y)
+    (default: eval_on_x + mle_eval); check_pairings=False skips the two mKZG pairing checks;
+    `out`, if a dict, receives the opening points (r_v padded, r_y) and challenges."""
     log_n = vk["log_n"]
     n = vk["n"]
     if fs is None:
         fs = Blake2s512Rng()
-    fs.feed(matrix_bytes(vk["A"], n))
-    fs.feed(matrix_bytes(vk["B"], n))
-    fs.feed(matrix_bytes(vk["C"], n))
+    if feed_matrices is not None:
+        feed_matrices(fs)
+    else:
+        fs.feed(matrix_bytes(vk["A"], n))
+        fs.feed(matrix_bytes(vk["B"], n))
+        fs.feed(matrix_bytes(vk["C"], n))
     fs.feed(vec_fr_bytes(v))
     if not is_pow2(len(v)) or len(v) > n:
         raise InvalidArgument("public input should be power of two and has size smaller than number of constraints")
@@ -653,7 +661,7 @@ def verify(vk, v, proof, vp, fs=None):
     com = proof.pm1
     z_rv_0, proof_rv = proof.pm2
     r_v0 = r_v + [0] * (log_n - log_v)
-    if not mkzg_verify(vp, com, r_v0, z_rv_0, proof_rv):
+    if check_pairings and not mkzg_verify(vp, com, r_v0, z_rv_0, proof_rv):
         raise InvalidArgument("public witness failed in commitment check")
     if mle_eval([x % R for x in v], r_v) != z_rv_0:
         raise InvalidArgument("public witness is inconsistent with proof")
@@ -667,12 +675,17 @@ def verify(vk, v, proof, vp, fs=None):
     z_ry, proof_ry = proof.pm6
     claimed2 = (r_a * va + r_b * vb + r_c * vc) % R
     r_y, expected2 = check_and_generate_subclaim(proof.sc2, rand2, claimed2, log_n, info2["max_multiplicands"])
-    a_rr = mle_eval(eval_on_x(vk["A"], r_x), r_y)
-    b_rr = mle_eval(eval_on_x(vk["B"], r_x), r_y)
-    c_rr = mle_eval(eval_on_x(vk["C"], r_x), r_y)
+    if eval_rr is not None:
+        a_rr, b_rr, c_rr = eval_rr(r_x, r_y)
+    else:
+        a_rr = mle_eval(eval_on_x(vk["A"], r_x), r_y)
+        b_rr = mle_eval(eval_on_x(vk["B"], r_x), r_y)
+        c_rr = mle_eval(eval_on_x(vk["C"], r_x), r_y)
     actual = (r_a * a_rr * z_ry + r_b * b_rr * z_ry + r_c * c_rr * z_ry) % R
     if expected2 != actual:
         raise WrongWitness("Cannot verify matrix A, B, C")
-    if not mkzg_verify(vp, com, r_y, z_ry, proof_ry):
+    if check_pairings and not mkzg_verify(vp, com, r_y, z_ry, proof_ry):
         raise WrongWitness("Cannot verify z_ry")
+    if out is not None:
+        out.update(r_v0=r_v0, r_y=r_y, r_x=r_x, tau=tau)
     return True

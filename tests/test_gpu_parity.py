@@ -126,3 +126,16 @@ def test_prove_many_concurrent(spx, ctx, oc, cached):
     assert len(got) == 7
     for g in got:
         assert g == want
+
+
+def test_prove_bit_exact_2_16(spx, ctx, oc):
+    """The largest bit-exact case vs the C oracle (2^16 constraints, ~30 s of oracle time); the PP
+    comes from the GPU keygen and is loaded into the oracle."""
+    log_n, log_v = 16, 5
+    inst = oc.Instance(0, log_n, log_v, 0x5EED0000 + log_n)
+    pp = spx.MLProofForR1CS.setup(ctx, log_n, 0xC0FFEE)
+    ppc = oc.PP.load(pp.serialize_uncompressed())
+    mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
+    pk = spx.MLArgumentForR1CS.index(ctx, *mats)
+    got = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+    assert got == oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)

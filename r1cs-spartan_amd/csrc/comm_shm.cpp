@@ -8,12 +8,16 @@
 // deadlock; a host allgather cannot. Latency is a few microseconds.
 //
 // Segment: [seq[r] (one cache line per rank)][2 buffers x world x kSlot bytes]. allgather #n writes
-// this rank's slot of buffer n&1, publishes seq[r] = n (release) and waits for every seq >= n
-// (acquire). Buffer n&1 is rewritten only by call n+2, which every rank starts after finishing call
-// n+1, i.e. after it has read call n's data.
+// this rank's slot of buffer n&1, publishes seq[r] = n (release), wakes futex waiters on it, and
+// waits for every seq >= n (acquire): a short spin, then a futex sleep on the peer's counter
+// (shared-mapping futexes work across processes), so hundreds of waiting proof threads on a node
+// do not steal cores from the ones hashing. Buffer n&1 is rewritten only by call n+2, which every
+// rank starts after finishing call n+1, i.e. after it has read call n's data.
 #include <fcntl.h>
+#include <linux/futex.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -64,25 +68,36 @@ struct ShmComm : Comm {
     ~ShmComm() override {
         if (base) munmap(base, len);
     }
-    std::atomic<uint64_t>& seq(int k) { return *reinterpret_cast<std::atomic<uint64_t>*>(base + 64 * k); }
-    uint8_t* slot(uint64_t call, int k) { return base + kHdr + ((call & 1) * w + k) * kSlot; }
+    // 32-bit counters (futex words); wrap-safe comparison
+    std::atomic<uint32_t>& seq(int k) { return *reinterpret_cast<std::atomic<uint32_t>*>(base + 64 * k); }
+    static bool reached(uint32_t v, uint32_t c) { return (int32_t)(v - c) >= 0; }
+    static void futex_wait(std::atomic<uint32_t>* a, uint32_t expect) {
+        struct timespec ts = {0, 2000000};  // 2 ms cap: re-check (and the 600 s deadline) periodically
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAIT, expect, &ts, nullptr, 0);
+    }
+    static void futex_wake(std::atomic<uint32_t>* a) {
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+    }
+    uint8_t* slot(uint32_t call, int k) { return base + kHdr + ((call & 1) * w + k) * kSlot; }
     int rank() const override { return r; }
     int size() const override { return w; }
     void one(const uint8_t* send, uint8_t* recv, size_t bytes, size_t rstride) {
-        const uint64_t c = ++n;
+        const uint32_t c = (uint32_t)++n;
         memcpy(slot(c, r), send, bytes);
         seq(r).store(c, std::memory_order_release);
+        futex_wake(&seq(r));
         auto t0 = std::chrono::steady_clock::now();
         for (int k = 0; k < w; ++k) {
             unsigned spins = 0;
-            while (seq(k).load(std::memory_order_acquire) < c) {
-                if (++spins < 4096) {
+            for (;;) {
+                const uint32_t v = seq(k).load(std::memory_order_acquire);
+                if (reached(v, c)) break;
+                if (++spins < 2048) {
                     __builtin_ia32_pause();
                     continue;
                 }
-                sched_yield();
-                if ((spins & 0xffff) == 0 &&
-                    std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
+                futex_wait(&seq(k), v);
+                if ((spins & 0xff) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
                     throw SpxError(kDevice, "shm allgather: rank " + std::to_string(k) + " did not arrive in 600 s");
             }
         }

@@ -555,7 +555,9 @@ static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
 }
 
 // ---------------------------------------------------------------- commit (commit.rs:17-29)
-static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
+// Split in two so the MSM runs while the host absorbs the matrices into the transcript: launch
+// enqueues the MSM and the copy of its XYZZ result into pinned memory; finish waits and decodes.
+static void commit_launch(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
     const uint64_t nl = n / G, lo = (uint64_t)rank * nl;
     MsmInst inst{};
     inst.pts_off = lo;
@@ -566,12 +568,17 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
     inst.W = (uint32_t)P.g1_W;
     void* out = C.buf(Ctx::kSlotCommit, 4 * sizeof(Fq));
     msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out, C.stream);
-    uint8_t* h = C.pinned(4 * sizeof(Fq));
-    SPX_HIP(hipMemcpyAsync(h, out, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(C.pinned(4 * sizeof(Fq)), out, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
+}
+static Affine<HFq> commit_finish(Ctx& C, int G) {
     C.sync();
-    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(h);
+    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(C.pinned(4 * sizeof(Fq)));
     if (G == 1) return part;
     return sum_affine(allgather_affine(*C.comm, part));
+}
+static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
+    commit_launch(C, P, z_full, n, G, rank);
+    return commit_finish(C, G);
 }
 
 // ---------------------------------------------------------------- open (open.rs:19-58)
@@ -714,34 +721,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     if (W.n != n) invalid("|v| + |w| != number of variables");  // prover.rs:117-119
     if (P.nv != L) invalid("public parameter nv != log_n");
     const int log_v = ilog2(nvv);
-    Transcript T(o.mode == 1, o.seed);
-    const uint64_t seq = C.prove_seq++;
-    if (o.cached && I.has_cache)
-        T.set_state(I.cache);
-    else if (G == 1) {
-        Blake2s h;
-        for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
-        T.set_state(h);
-    } else {
-        // the (sequential, ~150 MB at 2^20) absorption of A, B, C is done once per proof, by one rank
-        // in turn; the others take its Blake2s state from the allgather (bit-identical transcript)
-        static_assert(std::is_trivially_copyable<Blake2s>::value, "Blake2s state is shipped as bytes");
-        const int owner = (int)(seq % (uint64_t)G);
-        Blake2s h;
-        if (rank == owner)
-            for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
-        std::vector<uint8_t> all(sizeof(Blake2s) * G);
-        comm.allgather(&h, all.data(), sizeof(Blake2s));
-        memcpy(&h, all.data() + sizeof(Blake2s) * owner, sizeof(Blake2s));
-        T.set_state(h);
-    }
-    {
-        Ser s;
-        s.u64(nvv);
-        s.raw(W.v.data(), W.v.size());
-        T.feed(s.b.data(), s.b.size());
-    }
-    mark("transcript_matrices", tp);
     const Fr* z = W.z.as<Fr>();
     const Fr* zl = z + lo;
     // scratch layout (Fr units)
@@ -783,8 +762,37 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
                        I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
         kp_end(I.rows_bytes, C.stream);
     }
-    // ---- round 1: commitment (prover.rs:123-141)
-    Affine<HFq> com = commit_z(C, P, z, n, G, rank);
+    // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
+    commit_launch(C, P, z, n, G, rank);
+    Transcript T(o.mode == 1, o.seed);
+    const uint64_t seq = C.prove_seq++;
+    if (o.cached && I.has_cache)
+        T.set_state(I.cache);
+    else if (G == 1) {
+        Blake2s h;
+        for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        T.set_state(h);
+    } else {
+        // the (sequential, ~150 MB at 2^20) absorption of A, B, C is done once per proof, by one rank
+        // in turn; the others take its Blake2s state from the allgather (bit-identical transcript)
+        static_assert(std::is_trivially_copyable<Blake2s>::value, "Blake2s state is shipped as bytes");
+        const int owner = (int)(seq % (uint64_t)G);
+        Blake2s h;
+        if (rank == owner)
+            for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        std::vector<uint8_t> all(sizeof(Blake2s) * G);
+        comm.allgather(&h, all.data(), sizeof(Blake2s));
+        memcpy(&h, all.data() + sizeof(Blake2s) * owner, sizeof(Blake2s));
+        T.set_state(h);
+    }
+    {
+        Ser s;
+        s.u64(nvv);
+        s.raw(W.v.data(), W.v.size());
+        T.feed(s.b.data(), s.b.size());
+    }
+    mark("transcript_matrices", tp);
+    Affine<HFq> com = commit_finish(C, G);
     Ser proof;
     {
         size_t m0 = proof.b.size();

@@ -19,6 +19,11 @@
 // Many MSMs run as one batch (all nv levels of an opening): one pipeline, one sync.
 #include "msm_common.hpp"
 
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <cstdlib>
+
 namespace spx {
 
 __device__ __constant__ constexpr uint32_t kFqR2[12] = {0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u,
@@ -78,6 +83,18 @@ __global__ void k_seg_counts(const uint32_t* __restrict__ cnt, uint32_t nb, uint
 void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s) {
     const int gb = (int)((nb + 1 + kLight - 1) / kLight);
     hipLaunchKernelGGL(k_seg_counts, dim3(gb), dim3(kLight), 0, s, cnt, nb, segcnt, seg);
+}
+
+uint32_t seg1_len(bool g2) {
+    static const uint32_t v1 = [] {
+        const char* e = getenv("SPX_KSEG1");
+        return e ? (uint32_t)std::max(1, atoi(e)) : kSeg1Default;
+    }();
+    static const uint32_t v2 = [] {
+        const char* e = getenv("SPX_KSEG1_G2");
+        return e ? (uint32_t)std::max(1, atoi(e)) : v1;
+    }();
+    return g2 ? v2 : v1;
 }
 
 MsmWorkspace* msm_ws_create() { return new MsmWorkspace(); }

@@ -11,7 +11,8 @@
 
 namespace spx {
 
-static constexpr uint32_t kSeg1 = 32;  // references per thread, affine accumulation level
+static constexpr uint32_t kSeg1Default = 32;  // references per thread, affine accumulation level
+uint32_t seg1_len(bool g2);                      // kSeg1Default unless SPX_KSEG1 / SPX_KSEG1_G2 (tuning)
 static constexpr uint32_t kSeg = 32;    // partials per thread, XYZZ accumulation levels
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)

@@ -14,14 +14,15 @@ __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ off,
                                                       const uint32_t* __restrict__ cnt,
                                                       const uint32_t* __restrict__ refs,
-                                                      const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out) {
+                                                      const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out,
+                                                      uint32_t seg1) {
     using T = typename R29<F>::T;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= segoff[nb]) return;
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
-    const uint32_t start = off[b] + k * kSeg1;
-    const uint32_t end = min(start + kSeg1, off[b] + cnt[b]);
+    const uint32_t start = off[b] + k * seg1;
+    const uint32_t end = min(start + seg1, off[b] + cnt[b]);
     X29<T> acc;
     x29_set_inf(acc);
     for (uint32_t e = start; e < end; ++e) {
@@ -177,6 +178,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     const uint64_t tot_refs = so.tot_refs;
     // level 1: affine references -> XYZZ partials, one per segment of kSeg references
     const size_t psz = sizeof(Xyzz<F>);
+    const uint32_t kSeg1 = seg1_len(g2);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
@@ -184,7 +186,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     exclusive_scan(ws, so.segcnt, so.soa, nb + 1, s);
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((max_segs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.soa,
-                       nb, so.offs, so.counts, so.refs, pts, PA);
+                       nb, so.offs, so.counts, so.refs, pts, PA, kSeg1);
     // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
     kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s);
     uint32_t* cur_cnt = so.segcnt;

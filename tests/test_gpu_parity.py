@@ -54,6 +54,16 @@ def test_msm_repeated_scalar(spx, ctx, oc):
     assert spx.msm_g1(ctx, g1[: 96 * n], s * n) == oc.msm_g1(g1[: 96 * n], s * n, n)
 
 
+@pytest.mark.parametrize("scalar", [1, R - 1, 1 << 200])
+def test_msm_g2_degenerate_scalars(spx, ctx, oc, scalar):
+    """every scalar equal: each window's references pile into one bucket, past the capacity
+    layout's per-bucket slots, so the exact counting-sort fallback runs."""
+    n = 700
+    _, g2 = _pp_bases(oc, 10, 8)
+    s = scalar.to_bytes(32, "little")
+    assert spx.msm_g2(ctx, g2[: 192 * n], s * n) == oc.msm_g2(g2[: 192 * n], s * n, n)
+
+
 @pytest.mark.parametrize("nv", [3, 6])
 def test_keygen_matches_oracle(spx, ctx, oc, nv):
     pp = spx.MLProofForR1CS.setup(ctx, nv, 4242)

@@ -33,6 +33,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# measured VALU ceilings of the curve additions the MSM kernels run (tools/ubench29.hip with all 256 CUs
+# busy, profiles/r01_ubench29.txt): mixed additions per second
+MADD_CEILING = {"msm_acc_g2": 1.96e9, "msm_acc_g1": 5.78e9}
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
 KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
@@ -211,11 +214,13 @@ def main():
     stats = {}
     if not args.no_stats:
         for k, name in enumerate(KNAMES):
-            cnt, kms, by = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+            cnt, kms, by, ops = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
             spx._check(L.spx_kernel_stats(ctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
+            spx._check(L.spx_kernel_ops(ctx.h, k, ctypes.byref(ops)))
             if cnt.value:
                 # ctx 0 proves one proof per step
-                stats[name] = {"launches": cnt.value / args.steps, "ms": kms.value / args.steps, "bytes": by.value / args.steps}
+                stats[name] = {"launches": cnt.value / args.steps, "ms": kms.value / args.steps,
+                               "bytes": by.value / args.steps, "ops": ops.value / args.steps}
         spx._check(L.spx_kernel_stats_enable(ctx.h, 0))
     assert all(p == proofs[0] for p in proofs), "concurrent proofs differ"
     proof = proofs[0]
@@ -266,6 +271,19 @@ def main():
             "avg_launch_us": round(avg_s * 1e6, 2),
             "note": "algorithmic bytes / live HIP-event duration; MSM bucket accumulation is integer-VALU bound (see DESIGN.md)",
         }
+        if dom in MADD_CEILING and d["ops"]:
+            per_proof_ops = d["ops"]  # mixed additions of one proof
+            roof["valu"] = {
+                "unit": "mixed additions/s",
+                "ceiling": MADD_CEILING[dom],
+                "ceiling_source": "tools/ubench29.hip, all CUs busy (profiles/r01_ubench29.txt)",
+                # per launch, live duration (shares the GPU with the other proofs in flight)
+                "achieved_per_launch": round(d["ops"] / d["launches"] / avg_s, 1),
+                "frac_per_launch": round(d["ops"] / d["launches"] / avg_s / MADD_CEILING[dom], 4),
+                # whole job: this kernel's additions of every proof in the timed region / wall time
+                "achieved_job": round(per_proof_ops * B / (ms / 1e3), 1),
+                "frac_job": round(per_proof_ops * B / (ms / 1e3) / MADD_CEILING[dom], 4),
+            }
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds)

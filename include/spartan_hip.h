@@ -15,6 +15,7 @@
  * Reference interfaces replaced (file:line in /root/reference):
  *   spx_index            MLArgumentForR1CS::index                 src/lib.rs:45-51 -> src/ahp/indexer.rs:41-64
  *   spx_prove            MLArgumentForR1CS::prove                 src/lib.rs:58-146
+ *   spx_verify           MLArgumentForR1CS::verify                src/lib.rs:147-212
  *   spx_pp_load          PublicParameter (CanonicalDeserialize)   src/commitment/data_structures.rs:9-17
  *   spx_pp_generate      MLProofForR1CS::setup / MLPolyCommit::keygen  src/ahp/setup.rs:13-16, src/commitment/setup.rs:27-105
  *   spx_commit           MLPolyCommit::commit                     src/commitment/commit.rs:17-29
@@ -113,6 +114,18 @@ int spx_prove_witness(spx_ctx *ctx, spx_pk *idx, spx_witness *wit, spx_pp *pp, c
  * form of lib.rs:58-146 for a prover serving many witnesses; returns the first failure's status. */
 int spx_prove_many(spx_ctx **ctxs, int nctx, spx_pk *idx, spx_witness **wits, int nproofs, spx_pp *pp,
                    const spx_prove_opts *opts, uint8_t *out, size_t stride, size_t *lens);
+/* MLArgumentForR1CS::verify (src/lib.rs:147-212, verifier.rs:143-512): SPX_OK = accepted (the
+ * reference's Ok(true)); a rejection returns the reference's error kind (SPX_INVALID_ARGUMENT,
+ * SPX_SUMCHECK, SPX_WRONG_WITNESS, SPX_SERIALIZATION) with its message in spx_last_error.
+ * vp = VerifierParameter (commitment/data_structures.rs:19-26) in ark-serialize uncompressed form.
+ * The matrix evaluation runs on the ctx's GPU; the index must be built on a single-rank context. */
+int spx_verify(spx_ctx *ctx, spx_pk *idx, const uint8_t *v, size_t nv, const uint8_t *proof, size_t len,
+               const uint8_t *vp, size_t vp_len, const spx_prove_opts *opts);
+/* VerifierParameter of a keygen-generated PP (spx_pp_generate; setup.rs:91-101), uncompressed bytes */
+int spx_vp_from_pp(spx_pp *pp, uint8_t *out, size_t cap, size_t *len);
+/* prod_i e(P_i, Q_i) == 1 over n pairs (uncompressed G1 96 B / G2 192 B each); host only, no GPU
+ * (E::product_of_pairings as used by verify.rs:12-45) */
+int spx_pairing_check(const uint8_t *g1, const uint8_t *g2, size_t n, int *is_one);
 /* per-phase device timings of the last prove on this ctx, microseconds */
 int spx_last_timings(spx_ctx *ctx, double *out, int cap, int *n);
 
@@ -146,6 +159,9 @@ enum {
 };
 int spx_kernel_stats_enable(spx_ctx *ctx, int on);
 int spx_kernel_stats(spx_ctx *ctx, int id, uint64_t *launches, double *ms, double *bytes);
+/* unit operations counted for a kernel id: curve additions (upper bound: zero digits included) for
+ * SPX_K_ACC_* (mixed) and SPX_K_ACCX_* (XYZZ); 0 for the others */
+int spx_kernel_ops(spx_ctx *ctx, int id, double *ops);
 
 /* ---- kernel-level entry points (parity tests) ---- */
 int spx_sum_over_y(spx_ctx *ctx, const spx_csr *m, const uint8_t *z, uint8_t *out);

@@ -216,7 +216,8 @@ def check_and_generate_subclaim(msgs, randomness, asserted_sum, nv, max_mult):
         if len(evals) != max_mult + 1:
             raise InvalidArgument("wrong number of evaluations")
         if (evals[0] + evals[1]) % R != expected:
-            raise WrongWitness("Prover message is not consistent with the claim.")
+            # linear_sumcheck::Error, surfaced by the reference verifier's `?` as Error::SumCheckError
+            raise SumCheckError("Prover message is not consistent with the claim.")
         expected = interpolate_uni_poly(evals, r)
     return list(randomness), expected
 
@@ -280,6 +281,11 @@ class VerifierParameter:
         self.g = g
         self.h = h
         self.g_mask_random = g_mask_random
+
+    def serialize_uncompressed(self):
+        """CanonicalSerialize::serialize_uncompressed field order: nv, g, h, g_mask_random."""
+        return (ser_u64(self.nv) + g1_uncompressed(self.g) + g2_uncompressed(self.h) + ser_u64(len(self.g_mask_random))
+                + b"".join(g1_uncompressed(x) for x in self.g_mask_random))
 
 
 def _fixed_base_table(curve, base_aff, c, nwin):
@@ -405,13 +411,14 @@ def open_proof_bytes(proof):
 
 
 def mkzg_verify(vp, com, point, value, proof):
-    """verify.rs:12-45: e(C - g^v, h) == prod_i e(g^{t_i} - g^{p_i}, pi_i)."""
+    """verify.rs:12-45: e(C - g^v, vp.h) == prod_{i < vp.nv} e(g^{t_i} - g^{p_i}, pi_i) (the proof's own
+    h is not used, verify.rs:15)."""
     from pairing import product_of_pairings, is_one
 
     _nv, gp = com
-    h, proofs = proof
+    _h, proofs = proof
     left_pt = G1.to_affine(G1.add(G1.from_affine(gp), G1.neg(G1.mul(G1.from_affine(vp.g), value % R))))
-    pairs = [(left_pt, h)]
+    pairs = [(left_pt, vp.h)]
     for i in range(vp.nv):
         li = G1.add(G1.from_affine(vp.g_mask_random[i]), G1.neg(G1.mul(G1.from_affine(vp.g), point[i] % R)))
         pairs.append((G1.to_affine(G1.neg(li)), proofs[i]))

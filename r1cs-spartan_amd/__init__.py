@@ -94,6 +94,9 @@ EXPORTED = [
     "spx_prove_witness",
     "spx_prove_many",
     "spx_last_timings",
+    "spx_verify",
+    "spx_vp_from_pp",
+    "spx_pairing_check",
     "spx_sum_over_y",
     "spx_eval_on_x",
     "spx_msm_g1",
@@ -143,6 +146,9 @@ def lib():
     L.spx_prove_witness.argtypes = [vp, vp, vp, vp, ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_prove_many.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, ctypes.POINTER(vp), ctypes.c_int, vp,
                                  ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_verify.argtypes = [vp, vp, u8p, sz, u8p, sz, u8p, sz, ctypes.POINTER(_Opts)]
+    L.spx_vp_from_pp.argtypes = [vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.spx_pairing_check.argtypes = [u8p, u8p, sz, ctypes.POINTER(ctypes.c_int)]
     L.spx_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.spx_sum_over_y.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
     L.spx_eval_on_x.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
@@ -413,6 +419,34 @@ class MLArgumentForR1CS:
         _check(lib().spx_prove_many(ch, len(ctxs), pk.h, wh, n, pp.h, ctypes.byref(o), out, cap, lens))
         raw = out.raw
         return [raw[i * cap : i * cap + lens[i]] for i in range(n)]
+
+
+    @staticmethod
+    def verify(pk, v, proof, vp, mode="fs", seed=0, cached=False):
+        """lib.rs:147-212: True on acceptance; the reference's Err(...) raises the mapped exception."""
+        vb = _as_bytes(v)
+        o = _opts(mode, seed, cached)
+        _check(lib().spx_verify(pk.ctx.h, pk.h, vb, len(vb) // 32, bytes(proof), len(proof), bytes(vp), len(vp),
+                                ctypes.byref(o)))
+        return True
+
+
+def verifier_parameter(pp):
+    """VerifierParameter bytes (uncompressed) of a keygen-generated PP (setup.rs:91-101)."""
+    cap = 8 + 96 + 192 + 8 + 96 * 64
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    _check(lib().spx_vp_from_pp(pp.h, out, cap, ctypes.byref(n)))
+    return out.raw[: n.value]
+
+
+def pairing_product_is_one(g1_uncompressed, g2_uncompressed):
+    """prod_i e(P_i, Q_i) == 1 (host pairing; lists of uncompressed point bytes)."""
+    n = len(g1_uncompressed)
+    assert n == len(g2_uncompressed)
+    r = ctypes.c_int(0)
+    _check(lib().spx_pairing_check(b"".join(g1_uncompressed), b"".join(g2_uncompressed), n, ctypes.byref(r)))
+    return r.value == 1
 
 
 class MatrixExtension:

@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 
+#include "pairing.hpp"
 #include "prover.hpp"
 
 extern "C" int spx_comm_unique_id_impl(uint8_t out[128]);
@@ -270,6 +271,31 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     g_err.clear();
     return SPX_OK;
 }
+int spx_vp_from_pp(spx_pp* pp, uint8_t* out, size_t cap, size_t* len) {
+    return guard([&] {
+        if (!pp) spx::invalid("null public parameter");
+        copy_out(spx::vp_serialize(spx::vp_from_pp(*pp->p)), out, cap, len);
+    });
+}
+int spx_verify(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uint8_t* proof, size_t len,
+               const uint8_t* vp, size_t vp_len, const spx_prove_opts* opts) {
+    return guard([&] {
+        if (!idx || (nv && !v) || (len && !proof) || !vp) spx::invalid("null argument");
+        set_dev(ctx);
+        spx::verify(*ctx->c, *idx->i, v, nv, proof, len, spx::vp_load(vp, vp_len), opts_of(opts));
+    });
+}
+int spx_pairing_check(const uint8_t* g1, const uint8_t* g2, size_t n, int* is_one) {
+    return guard([&] {
+        if ((n && (!g1 || !g2)) || !is_one) spx::invalid("null argument");
+        std::vector<std::pair<spx::host::Affine<spx::host::Fq>, spx::host::Affine<spx::host::Fq2>>> pairs(n);
+        for (size_t i = 0; i < n; ++i)
+            if (!spx::host::g1_from_uncompressed(pairs[i].first, g1 + 96 * i) ||
+                !spx::host::g2_from_uncompressed(pairs[i].second, g2 + 192 * i))
+                throw spx::SpxError(spx::kSerialization, "bad point encoding");
+        *is_one = spx::host::pairing_product_is_one(pairs) ? 1 : 0;
+    });
+}
 int spx_last_timings(spx_ctx* ctx, double* out, int cap, int* n) {
     return guard([&] {
         auto& t = ctx->c->timings;
@@ -298,6 +324,14 @@ int spx_kernel_stats(spx_ctx* ctx, int id, uint64_t* launches, double* ms, doubl
     });
 }
 
+int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
+    return guard([&] {
+        if (id < 0 || id >= SPX_K_COUNT) spx::invalid("bad kernel id");
+        set_dev(ctx);
+        ctx->c->sync();
+        if (ops) *ops = ctx->c->kprof.ops[id];
+    });
+}
 int spx_sum_over_y(spx_ctx* ctx, const spx_csr* m, const uint8_t* z, uint8_t* out) {
     return guard([&] {
         set_dev(ctx);

@@ -40,12 +40,12 @@ struct KProf {
     struct Rec {
         int id;
         hipEvent_t a, b;
-        double bytes;
+        double bytes, ops;
     };
     std::vector<Rec> open;  // recorded, not yet harvested
     std::vector<hipEvent_t> pool;
     uint64_t launches[16] = {0};
-    double ms[16] = {0}, bytes[16] = {0};
+    double ms[16] = {0}, bytes[16] = {0}, ops[16] = {0};
     int cur_id = -1;
     hipEvent_t cur_a = nullptr;
     hipEvent_t get() {
@@ -64,11 +64,11 @@ struct KProf {
         cur_a = get();
         (void)hipEventRecord(cur_a, s);
     }
-    void end(double algo_bytes, hipStream_t s) {
+    void end(double algo_bytes, hipStream_t s, double n_ops) {
         if (!on || cur_id < 0) return;
         hipEvent_t b = get();
         (void)hipEventRecord(b, s);
-        open.push_back({cur_id, cur_a, b, algo_bytes});
+        open.push_back({cur_id, cur_a, b, algo_bytes, n_ops});
         cur_id = -1;
     }
     void harvest() {  // call after a stream sync
@@ -78,6 +78,7 @@ struct KProf {
                 launches[r.id] += 1;
                 ms[r.id] += t;
                 bytes[r.id] += r.bytes;
+                ops[r.id] += r.ops;
             }
             pool.push_back(r.a);
             pool.push_back(r.b);
@@ -85,15 +86,17 @@ struct KProf {
         open.clear();
     }
     void reset() {
-        for (int i = 0; i < 16; ++i) launches[i] = 0, ms[i] = 0, bytes[i] = 0;
+        for (int i = 0; i < 16; ++i) launches[i] = 0, ms[i] = 0, bytes[i] = 0, ops[i] = 0;
     }
 };
 extern thread_local KProf* g_kprof;  // set by the host for the calling thread
 inline void kp_begin(int id, hipStream_t s) {
     if (g_kprof) g_kprof->begin(id, s);
 }
-inline void kp_end(double bytes, hipStream_t s) {
-    if (g_kprof) g_kprof->end(bytes, s);
+// bytes: algorithmic bytes of the launch; ops: its unit operations (curve additions for the MSM
+// levels, table entries elsewhere; 0 where no op count is defined)
+inline void kp_end(double bytes, hipStream_t s, double ops = 0) {
+    if (g_kprof) g_kprof->end(bytes, s, ops);
 }
 enum { KP_SC1 = 0, KP_SC2, KP_SPMV, KP_MTV, KP_OPEN, KP_EQ, KP_SORT, KP_ACC_G1, KP_ACC_G2, KP_ACCX_G1, KP_ACCX_G2,
        KP_RED_G1, KP_RED_G2 };

@@ -188,7 +188,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((max_segs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.soa,
                        nb, so.offs, so.counts, so.refs, pts, PA, kSeg1);
     // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
-    kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s);
+    kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s, (double)tot_refs);
     uint32_t* cur_cnt = so.segcnt;
     uint32_t* cur_off = so.soa;
     uint32_t* nxt_off = so.sob;
@@ -204,7 +204,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
         hipLaunchKernelGGL(k_accum_xyzz<F>, dim3((unsigned)((nsegs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
                            nxt_off, nb, cur_off, cur_cnt, cur, nxt);
-        kp_end((double)(cur_max_segs + nsegs) * psz, s);
+        kp_end((double)(cur_max_segs + nsegs) * psz, s, (double)cur_max_segs);
         std::swap(cur, nxt);
         std::swap(cur_off, nxt_off);
         std::swap(cur_cnt, spare_cnt);

@@ -7,6 +7,7 @@
 // round exchanges 3 Fr per rank, each MSM one affine point per rank. The last g rounds/levels run on
 // the gathered G-entry tables. Every rank replays the same transcript, so no challenge broadcast.
 #include "prover.hpp"
+#include "pairing.hpp"
 
 #include <type_traits>
 
@@ -1043,6 +1044,306 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
 }
 
 // ====================================================================== kernel-level entry points
+// ====================================================================== verifier
+// lib.rs:147-212 with verifier.rs:143-512. The transcript is replayed on the host; the O(nnz) matrix
+// evaluation (A, B, C)(r_x, r_y) runs on the GPU with the prover's kernels (eq table, CSC gather into
+// sum_M r_M M(r_x, .), then L fold levels at r_y); the two mKZG checks (verify.rs:12-45) use the
+// host pairing of pairing.hpp.
+VP vp_load(const uint8_t* b, size_t len) {
+    VP V;
+    size_t pos = 0;
+    auto take = [&](size_t k) {
+        if (pos + k > len) throw SpxError(kSerialization, "truncated verifier parameter");
+        const uint8_t* p = b + pos;
+        pos += k;
+        return p;
+    };
+    uint64_t nv, cnt;
+    memcpy(&nv, take(8), 8);
+    if (nv > 40) throw SpxError(kSerialization, "bad verifier parameter nv");
+    V.nv = (int)nv;
+    if (!host::g1_from_uncompressed(V.g, take(96)) || !host::g2_from_uncompressed(V.h, take(192)))
+        throw SpxError(kSerialization, "bad verifier parameter point");
+    memcpy(&cnt, take(8), 8);
+    if (cnt != nv) throw SpxError(kSerialization, "g_mask_random length != nv");
+    V.g_mask.resize(cnt);
+    for (auto& g : V.g_mask)
+        if (!host::g1_from_uncompressed(g, take(96))) throw SpxError(kSerialization, "bad g_mask_random point");
+    if (pos != len) throw SpxError(kSerialization, "trailing bytes in verifier parameter");
+    return V;
+}
+std::vector<uint8_t> vp_serialize(const VP& V) {
+    Ser s;
+    s.u64((uint64_t)V.nv);
+    uint8_t b[192];
+    host::g1_to_uncompressed(b, V.g);
+    s.raw(b, 96);
+    host::g2_to_uncompressed(b, V.h);
+    s.raw(b, 192);
+    s.u64(V.g_mask.size());
+    for (auto& g : V.g_mask) {
+        host::g1_to_uncompressed(b, g);
+        s.raw(b, 96);
+    }
+    return s.b;
+}
+VP vp_from_pp(const PP& P) {
+    if (!P.has_t) invalid("verifier parameter needs a keygen-generated PP (trapdoor unknown)");
+    VP V;
+    V.nv = P.nv;
+    V.g = P.g;
+    V.h = P.h;
+    for (int i = 0; i < P.nv; ++i) {  // setup.rs:91-101: g_mask_random[i] = g^{t_i}
+        uint64_t k[4];
+        P.t[i].to_canon(k);
+        V.g_mask.push_back(host::jac_to_affine(host::jac_mul(host::jac_from(P.g), k)));
+    }
+    return V;
+}
+
+namespace {
+struct ProofReader {
+    const uint8_t* b;
+    size_t len, pos = 0;
+    const uint8_t* take(size_t k) {
+        if (pos + k > len) throw SpxError(kSerialization, "truncated proof");
+        const uint8_t* p = b + pos;
+        pos += k;
+        return p;
+    }
+    uint64_t u64() {
+        uint64_t v;
+        memcpy(&v, take(8), 8);
+        return v;
+    }
+    HFr fr() {
+        HFr r;
+        if (!host::fr_from_bytes(r, take(32))) throw SpxError(kSerialization, "non-canonical field element");
+        return r;
+    }
+    host::Affine<HFq> g1() {
+        host::Affine<HFq> a;
+        if (!host::g1_decompress(a, take(48))) throw SpxError(kSerialization, "invalid G1 point");
+        return a;
+    }
+    host::Affine<HFq2> g2() {
+        host::Affine<HFq2> a;
+        if (!host::g2_decompress(a, take(96))) throw SpxError(kSerialization, "invalid G2 point");
+        return a;
+    }
+};
+struct OpenProof {
+    HFr eval;
+    host::Affine<HFq2> h;
+    std::vector<host::Affine<HFq2>> proofs;
+};
+OpenProof read_open(ProofReader& R) {
+    OpenProof o;
+    o.eval = R.fr();
+    o.h = R.g2();
+    const uint64_t k = R.u64();
+    if (k > 64) throw SpxError(kSerialization, "bad opening proof length");
+    for (uint64_t i = 0; i < k; ++i) o.proofs.push_back(R.g2());
+    return o;
+}
+std::vector<std::vector<HFr>> read_msgs(ProofReader& R, std::vector<std::pair<size_t, size_t>>& spans) {
+    const uint64_t rounds = R.u64();
+    if (rounds > 64) throw SpxError(kSerialization, "bad sumcheck round count");
+    std::vector<std::vector<HFr>> m(rounds);
+    for (auto& e : m) {
+        const size_t start = R.pos;
+        const uint64_t k = R.u64();
+        if (k > 1024) throw SpxError(kSerialization, "bad sumcheck message length");
+        for (uint64_t i = 0; i < k; ++i) e.push_back(R.fr());
+        spans.emplace_back(start, R.pos - start);
+    }
+    return m;
+}
+// linear-sumcheck interpolate_uni_poly: value at x of the polynomial through (i, ev[i])
+HFr interpolate(const std::vector<HFr>& ev, const HFr& x) {
+    const size_t n = ev.size();
+    HFr total = HFr::zero();
+    for (size_t i = 0; i < n; ++i) {
+        HFr num = HFr::one(), den = HFr::one();
+        for (size_t j = 0; j < n; ++j) {
+            if (j == i) continue;
+            num = num * (x - HFr::from_u64(j));
+            den = den * (HFr::from_u64(i) - HFr::from_u64(j));
+        }
+        total = total + ev[i] * num * den.inv();
+    }
+    return total;
+}
+// linear-sumcheck check_and_generate_subclaim; its errors surface as Error::SumCheckError
+HFr check_subclaim(const std::vector<std::vector<HFr>>& msgs, const std::vector<HFr>& rnd, HFr expected, int nv,
+                   uint64_t max_mult) {
+    if ((int)msgs.size() != nv) throw SpxError(kSumcheck, "insufficient rounds");
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        if (msgs[i].size() != max_mult + 1) throw SpxError(kSumcheck, "wrong number of evaluations");
+        if (!(msgs[i][0] + msgs[i][1] == expected))
+            throw SpxError(kSumcheck, "Prover message is not consistent with the claim.");
+        expected = interpolate(msgs[i], rnd[i]);
+    }
+    return expected;
+}
+// MLPolyCommit::verify (verify.rs:12-45), vp.h on the left as in the reference
+bool mkzg_check(const VP& V, const host::Affine<HFq>& com, const std::vector<HFr>& point, const HFr& value,
+                const OpenProof& op) {
+    if ((int)op.proofs.size() < V.nv || (int)point.size() < V.nv) return false;
+    using host::jac_add;
+    using host::jac_from;
+    using host::jac_mul;
+    using host::jac_to_affine;
+    auto neg = [](host::Affine<HFq> a) {
+        a.y = -a.y;
+        return a;
+    };
+    uint64_t k[4];
+    value.to_canon(k);
+    std::vector<std::pair<host::Affine<HFq>, host::Affine<HFq2>>> pairs;
+    pairs.push_back({jac_to_affine(jac_add(jac_from(com), jac_from(neg(jac_to_affine(jac_mul(jac_from(V.g), k)))))),
+                     V.h});
+    for (int i = 0; i < V.nv; ++i) {
+        point[i].to_canon(k);
+        host::Affine<HFq> li = jac_to_affine(
+            jac_add(jac_from(V.g_mask[i]), jac_from(neg(jac_to_affine(jac_mul(jac_from(V.g), k))))));
+        if (!li.inf) li = neg(li);
+        pairs.push_back({li, op.proofs[i]});
+    }
+    return host::pairing_product_is_one(pairs);
+}
+HFr mle_eval_host(std::vector<HFr> t, const std::vector<HFr>& point) {
+    for (const HFr& r : point) {
+        std::vector<HFr> nt(t.size() / 2);
+        for (size_t b = 0; b < nt.size(); ++b) nt[b] = t[2 * b] + r * (t[2 * b + 1] - t[2 * b]);
+        t.swap(nt);
+    }
+    return t[0];
+}
+}  // namespace
+
+// sum_M r_M M(r_x, r_y) on the GPU: eq(r_x) table, CSC gather (the prover's eval_on_x pass), L folds
+static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const HFr rabc[3],
+                            const std::vector<HFr>& r_y) {
+    const int L = I.log_n;
+    const uint64_t n = I.n;
+    const uint64_t parts = std::max<uint64_t>(3 * 2048, (uint64_t)I.cols.nchunks);
+    C.scratch.ensure(32 * (n + n + n / 2 + 2 + parts + 8192 * 2 + 4 * L + 8));
+    Fr* base = C.scratch.as<Fr>();
+    Fr *EQ = base, *M0 = EQ + n, *Mb = M0 + n, *partial = Mb + n / 2 + 2, *eqlo = partial + parts, *eqhi = eqlo + 8192;
+    Fr* ch = eqhi + 8192;  // r_x (L), r_abc (3), r_y (L)
+    std::vector<HFr> hch(r_x);
+    hch.insert(hch.end(), rabc, rabc + 3);
+    hch.insert(hch.end(), r_y.begin(), r_y.end());
+    SPX_HIP(hipMemcpyAsync(ch, hch.data(), 32 * hch.size(), hipMemcpyHostToDevice, C.stream));  // pageable: staged
+    launch_eq_table(ch, L, 0, n, EQ, eqlo, eqhi, C.stream);
+    SparseView3 cv = I.cols.view();
+    launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, ch + L, n, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
+                   I.cols.lrows.as<LongRow>(), I.cols.nlrows, partial, C.stream);
+    // fold at r_y (variable 0 = LSB): M0 -> EQ (as q scratch) / Mb ping-pong
+    const Fr* rin = M0;
+    Fr* bufs[2] = {Mb, M0};
+    for (int i = 0; i < L; ++i) {
+        const uint64_t half = n >> (i + 1);
+        Fr* rout = bufs[i & 1];
+        launch_open_level(rin, rout, EQ, ch + L + 3 + i, half, C.stream);
+        rin = rout;
+    }
+    uint8_t* hp = C.pinned(32);
+    SPX_HIP(hipMemcpyAsync(hp, rin, 32, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    return ld_hfr(hp);
+}
+
+void verify(Ctx& C, Index& I, const uint8_t* v, size_t nv, const uint8_t* proof, size_t len, const VP& V,
+            const ProveOpts& o) {
+    if (I.G != 1) invalid("verify needs an index built on a single-rank context");
+    const int L = I.log_n;
+    const uint64_t n = I.n;
+    // verifier_init (verifier.rs:143-146)
+    if (!is_pow2(nv) || nv > n)
+        invalid("public input should be power of two and has size smaller than number of constraints");
+    const int log_v = ilog2(nv);
+    std::vector<HFr> vv(nv);
+    for (size_t i = 0; i < nv; ++i)
+        if (!host::fr_from_bytes(vv[i], v + 32 * i)) invalid("public input is not a canonical field element");
+    // parse (proof.rs:10-20 field order); remember each message's byte span for the transcript
+    ProofReader R{proof, len};
+    const size_t pm1_at = R.pos;
+    const uint64_t com_nv = R.u64();
+    const host::Affine<HFq> com = R.g1();
+    const size_t pm1_len = R.pos - pm1_at, pm2_at = R.pos;
+    const OpenProof op1 = read_open(R);
+    const size_t pm2_len = R.pos - pm2_at, pm3_at = R.pos;
+    const uint64_t mm1 = R.u64(), nv1 = R.u64();
+    std::vector<std::pair<size_t, size_t>> sp1, sp2;
+    const auto sc1 = read_msgs(R, sp1);
+    const size_t pm4_at = R.pos;
+    const HFr va = R.fr(), vb = R.fr(), vc = R.fr();
+    const size_t pm5_at = R.pos;
+    const uint64_t mm2 = R.u64(), nv2 = R.u64();
+    const auto sc2 = read_msgs(R, sp2);
+    const size_t pm6_at = R.pos;
+    const OpenProof op2 = read_open(R);
+    const size_t pm6_len = R.pos - pm6_at;
+    if (R.pos != len) throw SpxError(kSerialization, "trailing bytes in proof");
+    (void)com_nv;
+    // transcript (lib.rs:152-212 feed order)
+    Transcript T(o.mode == 1, o.seed);
+    if (o.cached && I.has_cache)
+        T.set_state(I.cache);
+    else {
+        Blake2s h;
+        for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        T.set_state(h);
+    }
+    {
+        Ser s;
+        s.u64(nv);
+        s.raw(v, 32 * nv);
+        T.feed(s.b.data(), s.b.size());
+    }
+    T.feed(proof + pm1_at, pm1_len);
+    std::vector<HFr> r_v(log_v);
+    for (auto& r : r_v) r = T.rand_fr();
+    T.feed(proof + pm2_at, pm2_len);
+    std::vector<HFr> tau(L);
+    for (auto& t : tau) t = T.rand_fr();
+    if (nv1 != (uint64_t)L) invalid("invalid sumcheck proposal");
+    T.feed(proof + pm3_at, 16);
+    if ((int)sc1.size() != L || (int)sc2.size() != L) invalid("malformed sumcheck message");
+    std::vector<HFr> rand1, rand2;
+    for (auto& sp : sp1) {
+        T.feed(proof + sp.first, sp.second);
+        rand1.push_back(T.rand_fr());
+    }
+    T.feed(proof + pm4_at, 96);
+    const HFr r_a = T.rand_fr(), r_b = T.rand_fr(), r_c = T.rand_fr();
+    if (nv2 != (uint64_t)L) invalid("invalid sumcheck proposal");
+    T.feed(proof + pm5_at, 16);
+    for (auto& sp : sp2) {
+        T.feed(proof + sp.first, sp.second);
+        rand2.push_back(T.rand_fr());
+    }
+    T.feed(proof + pm6_at, pm6_len);
+    // verify_sixth_round (verifier.rs:443-512)
+    if (V.nv != L) invalid("verifier parameter nv != log_n");
+    std::vector<HFr> r_v0(L, HFr::zero());
+    for (int i = 0; i < log_v; ++i) r_v0[i] = r_v[i];
+    if (!mkzg_check(V, com, r_v0, op1.eval, op1)) invalid("public witness failed in commitment check");
+    if (!(mle_eval_host(vv, r_v) == op1.eval)) invalid("public witness is inconsistent with proof");
+    const HFr expected1 = check_subclaim(sc1, rand1, HFr::zero(), L, mm1);
+    HFr eq_rx = HFr::one();
+    for (int i = 0; i < L; ++i) eq_rx = eq_rx * eq1(tau[i], rand1[i]);
+    if (!((va * vb - vc) * eq_rx == expected1)) throw SpxError(kWrongWitness, "first sumcheck has wrong subclaim");
+    const HFr claimed2 = r_a * va + r_b * vb + r_c * vc;
+    const HFr expected2 = check_subclaim(sc2, rand2, claimed2, L, mm2);
+    const HFr rabc[3] = {r_a, r_b, r_c};
+    const HFr actual = eval_matrices_at(C, I, rand1, rabc, rand2) * op2.eval;
+    if (!(expected2 == actual)) throw SpxError(kWrongWitness, "Cannot verify matrix A, B, C");
+    if (!mkzg_check(V, com, rand2, op2.eval, op2)) throw SpxError(kWrongWitness, "Cannot verify z_ry");
+}
+
 static HostCsr single(const HostCsr& m) { return m; }
 
 std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z) {

@@ -218,6 +218,21 @@ std::unique_ptr<Witness> witness_upload(Ctx& C, const uint8_t* v, size_t nv, con
 std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts& o);
 size_t proof_size(int log_n);
 
+// verifier (lib.rs:147-212 with verifier.rs:143-512); VerifierParameter: data_structures.rs:19-26
+struct VP {
+    int nv = 0;
+    host::Affine<host::Fq> g;
+    host::Affine<host::Fq2> h;
+    std::vector<host::Affine<host::Fq>> g_mask;  // g^{t_i}
+};
+VP vp_load(const uint8_t* b, size_t len);
+std::vector<uint8_t> vp_serialize(const VP& V);
+VP vp_from_pp(const PP& P);  // keygen-generated PP only (keeps the trapdoor)
+// throws SpxError(kInvalidArgument / kSumcheck / kWrongWitness / kSerialization) on rejection, as the
+// reference's Err(...); returns normally on acceptance (Ok(true))
+void verify(Ctx& C, Index& I, const uint8_t* v, size_t nv, const uint8_t* proof, size_t len, const VP& V,
+            const ProveOpts& o);
+
 std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z);
 std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x);
 std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t* scalars, size_t n);

@@ -89,6 +89,12 @@ def test_fullsize_2_20(spx, ctx):
         spartan.verify({"log_n": log_n, "n": n}, z[: 1 << log_v], bad, None, feed_matrices=feed, eval_rr=eval_rr,
                        check_pairings=False)
 
+    # the product's verifier (GPU eval_on_x + host pairings) accepts it, and rejects the corrupted one
+    vp = spx.verifier_parameter(pp)
+    assert spx.MLArgumentForR1CS.verify(pk, zb[: 32 << log_v], proof, vp)
+    with pytest.raises((spx.SumCheckError, spx.WrongWitness)):
+        spx.MLArgumentForR1CS.verify(pk, zb[: 32 << log_v], bad.to_bytes(), vp)
+
     # commitment and openings against the trapdoor (draw order g, h, t: setup.rs:28-34)
     rng = SplitMix64(pp_seed)
     gs, hs = rng.next_fr(), rng.next_fr()

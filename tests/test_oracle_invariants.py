@@ -11,6 +11,7 @@ from gen import SplitMix64, random_matrix, ref_shaped, uniform_3n
 from pairing import pairing, f12_mul, ONE12
 from spartan import (
     Proof,
+    SumCheckError,
     WrongWitness,
     InvalidArgument,
     commit,
@@ -122,7 +123,7 @@ def test_wrong_witness_and_tampering_rejected():
     pk = index(A, B, C)
     w2 = list(w)
     w2[3] = (w2[3] + 1) % R
-    with pytest.raises((WrongWitness, InvalidArgument)):
+    with pytest.raises((WrongWitness, InvalidArgument, SumCheckError)):
         verify(pk, v, prove(pk, v, w2, pp), vp)
     b = bytearray(prove(pk, v, w, pp).to_bytes())
     b[200] ^= 1  # inside the z(r_v, 0) opening proof / sumcheck messages

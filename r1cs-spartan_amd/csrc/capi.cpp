@@ -4,6 +4,10 @@
 #include "../../include/spartan_hip.h"
 
 #include <atomic>
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <condition_variable>
 #include <memory>
 #include <string>
 #include <thread>
@@ -239,13 +243,71 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             g_err = "spx_prove_many: null witness";
             return SPX_INVALID_ARGUMENT;
         }
-    const spx::ProveOpts o = opts_of(opts);
+    spx::ProveOpts base;
+    try {
+        base = opts_of(opts);
+    } catch (const spx::SpxError& e) {
+        g_err = e.what();
+        return e.code;
+    }
+    // Proof i is absorbed (A, B, C into its transcript) by rank i mod G, on a pool of host threads
+    // that runs ahead of the GPU workers: the sequential ~150 MB Blake2s pass of each proof overlaps
+    // the device work of earlier proofs instead of sitting in front of its own. Every proof is still
+    // absorbed exactly once; only the schedule changes.
+    const int G = ctxs[0]->c->comm->size(), rank = ctxs[0]->c->comm->rank();
+    struct Slot {
+        std::atomic<int> state{0};  // 0 pending, 1 ready, 2 failed
+        spx::Blake2s h;
+    };
+    std::vector<Slot> slots(base.cached ? 0 : nproofs);
+    std::vector<int> owned;
+    if (!base.cached)
+        for (int i = 0; i < nproofs; ++i)
+            if (i % G == rank) owned.push_back(i);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<size_t> next_job{0};
+    std::string pool_err;
+    auto hasher = [&] {
+        for (;;) {
+            const size_t j = next_job.fetch_add(1);
+            if (j >= owned.size()) return;
+            Slot& sl = slots[owned[j]];
+            int st = 1;
+            try {
+                sl.h = spx::absorb_matrices(*idx->i);
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(mu);
+                pool_err = e.what();
+                st = 2;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                sl.state.store(st);
+            }
+            cv.notify_all();
+        }
+    };
+    int nh = nctx;
+    if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
+    nh = std::min<int>(nh, (int)owned.size());
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nh; ++t) pool.emplace_back(hasher);
+
     std::vector<int> st(nctx, SPX_OK);
     std::vector<std::string> msg(nctx);
     auto work = [&](int k) {
         for (int i = k; i < nproofs; i += nctx) {
             int rc = guard([&] {
                 set_dev(ctxs[k]);
+                spx::ProveOpts o = base;
+                o.seq = i;
+                if (!base.cached && i % G == rank) {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return slots[i].state.load() != 0; });
+                    if (slots[i].state.load() == 2) throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
+                    o.absorbed = &slots[i].h;
+                }
                 auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, *pp->p, o);
                 if (p.size() > stride) spx::invalid("proof buffer too small");
                 memcpy(out + (size_t)i * stride, p.data(), p.size());
@@ -263,6 +325,8 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     for (int k = 1; k < nw; ++k) th.emplace_back(work, k);
     work(0);
     for (auto& t : th) t.join();
+    next_job.store(owned.size());  // stop a pool still running after a worker failure
+    for (auto& t : pool) t.join();
     for (int k = 0; k < nw; ++k)
         if (st[k] != SPX_OK) {
             g_err = msg[k];

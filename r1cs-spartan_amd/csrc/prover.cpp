@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace spx {
@@ -24,6 +25,13 @@ using HFq2 = host::Fq2;
 
 // ====================================================================== context
 Ctx::Ctx(int dev) : device(dev) {
+    // SPX_BLOCKING_SYNC=1: host waits sleep instead of spinning (frees cores for the transcript
+    // hashing pool when many proofs are in flight); must precede the device's first use
+    static const bool blocking = [] {
+        const char* e = getenv("SPX_BLOCKING_SYNC");
+        return e && e[0] == '1';
+    }();
+    if (blocking) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     SPX_HIP(hipSetDevice(dev));
     SPX_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     msm = msm_ws_create();
@@ -399,6 +407,12 @@ static void feed_matrix(Blake2s& h, const HostCsr& m) {
     flush();
 }
 
+Blake2s absorb_matrices(const Index& I) {
+    Blake2s h;
+    for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+    return h;
+}
+
 std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
     auto I = std::make_unique<Index>();
     const uint64_t n = mats[0].n;
@@ -766,21 +780,19 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
     commit_launch(C, P, z, n, G, rank);
     Transcript T(o.mode == 1, o.seed);
-    const uint64_t seq = C.prove_seq++;
+    const uint64_t ctr = C.prove_seq++;
+    const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
     if (o.cached && I.has_cache)
         T.set_state(I.cache);
     else if (G == 1) {
-        Blake2s h;
-        for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
-        T.set_state(h);
+        T.set_state(o.absorbed ? *o.absorbed : absorb_matrices(I));
     } else {
         // the (sequential, ~150 MB at 2^20) absorption of A, B, C is done once per proof, by one rank
         // in turn; the others take its Blake2s state from the allgather (bit-identical transcript)
         static_assert(std::is_trivially_copyable<Blake2s>::value, "Blake2s state is shipped as bytes");
         const int owner = (int)(seq % (uint64_t)G);
         Blake2s h;
-        if (rank == owner)
-            for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
+        if (rank == owner) h = o.absorbed ? *o.absorbed : absorb_matrices(I);
         std::vector<uint8_t> all(sizeof(Blake2s) * G);
         comm.allgather(&h, all.data(), sizeof(Blake2s));
         memcpy(&h, all.data() + sizeof(Blake2s) * owner, sizeof(Blake2s));

@@ -207,7 +207,12 @@ struct ProveOpts {
     int mode = 0;
     uint64_t seed = 0;
     bool cached = false;
+    // scheduling hooks used by spx_prove_many (neither changes the proof):
+    int64_t seq = -1;                 // proof number deciding which rank absorbs A, B, C (default: ctx counter)
+    const Blake2s* absorbed = nullptr;  // this proof's A, B, C absorption, already computed by the caller
 };
+// Blake2s state after absorbing A, B, C (lib.rs:61-64): the per-proof sequential host work
+Blake2s absorb_matrices(const Index& I);
 
 // entry points used by the C ABI
 std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len);

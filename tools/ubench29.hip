@@ -76,17 +76,26 @@ __global__ __launch_bounds__(64) void k_madd_thr(Xyzz<S>* acc, const Aff<S>* pts
         acc[i] = a;
     }
 }
+// two waves per SIMD forced (<= 256 VGPRs)
+template <class S>
+__global__ __launch_bounds__(64, 2) void k_madd_thr_o2(Xyzz<S>* acc, const Aff<S>* pts, int npts, int iters) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    using T = typename R29<S>::T;
+    X29<T> A; ld29<S>(A, acc + i);
+    for (int k = 0; k < iters; ++k) { A29<T> p; ld29<S>(p, pts + (i + k * 977) % npts); x29_madd(A, p.x, p.y, (k & 1) != 0); }
+    st29<S>(acc + i, A);
+}
 template <class S, int NEW>
 __global__ __launch_bounds__(64) void k_add_lat(Xyzz<S>* acc, const Xyzz<S>* q, int iters) {
     if (NEW) {
         using T = typename R29<S>::T;
-        X29<T> A; ld29<S>(A, acc);
-        for (int k = 0; k < iters; ++k) { X29<T> B; ld29<S>(B, q + (k & 7)); x29_add(A, B); }
-        st29<S>(acc, A);
+        X29<T> A; ld29<S>(A, acc + threadIdx.x);
+        for (int k = 0; k < iters; ++k) { X29<T> B; ld29<S>(B, q + ((k + threadIdx.x) & 63)); x29_add(A, B); }
+        st29<S>(acc + threadIdx.x, A);
     } else {
-        Xyzz<S> a = acc[0];
-        for (int k = 0; k < iters; ++k) xyzz_add(a, q[k & 7]);
-        acc[0] = a;
+        Xyzz<S> a = acc[threadIdx.x];
+        for (int k = 0; k < iters; ++k) xyzz_add(a, q[(k + threadIdx.x) & 63]);
+        acc[threadIdx.x] = a;
     }
 }
 __global__ void k_fq_thr29(F29* out, const F29* in, int iters) {
@@ -158,6 +167,8 @@ int main() {
     printf("G2 madd 32  : %.3f G/s\n", (double)nth * it / t / 1e6);
     t = timeit([&] { hipLaunchKernelGGL((k_madd_thr<Fq2, 1>), dim3(nth / 64), dim3(64), 0, 0, (G2Xyzz*)tacc, (const G2Aff*)tpts, npts, it); });
     printf("G2 madd 29  : %.3f G/s\n", (double)nth * it / t / 1e6);
+    t = timeit([&] { hipLaunchKernelGGL((k_madd_thr_o2<Fq2>), dim3(nth / 64), dim3(64), 0, 0, (G2Xyzz*)tacc, (const G2Aff*)tpts, npts, it); });
+    printf("G2 madd 29 occ2: %.3f G/s\n", (double)nth * it / t / 1e6);
     it = 100;
     t = timeit([&] { hipLaunchKernelGGL((k_add_lat<Fq2, 0>), dim3(1), dim3(64), 0, 0, (G2Xyzz*)tacc, (const G2Xyzz*)tacc + 64, it); });
     printf("G2 add lat 32: %.1f us\n", t * 1e3 / it);

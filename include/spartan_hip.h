@@ -129,6 +129,30 @@ int spx_pairing_check(const uint8_t *g1, const uint8_t *g2, size_t n, int *is_on
 /* per-phase device timings of the last prove on this ctx, microseconds */
 int spx_last_timings(spx_ctx *ctx, double *out, int cap, int *n);
 
+/* ---- R1CS front-end: ark-relations ConstraintSystem semantics ----
+ * Variable 0 is the constant One; spx_cs_new_input returns instance variables (Variable::Instance,
+ * numbered before witnesses in z = v || w), spx_cs_new_witness returns witness variables (bit 63
+ * set). Linear combinations are compactified on export (sorted, merged, zeros dropped:
+ * LinearCombination::compactify / inline_all_lcs). spx_cs_make_square follows test_utils.rs:81-102.
+ * spx_cs_matrices exports CSR rows (constraints) over columns z and v / w value bytes, valid until
+ * the next change to the system; they feed spx_index and spx_prove directly. Host only. */
+typedef struct spx_cs spx_cs;
+typedef struct {
+    const uint64_t *vars;    /* len variables */
+    const uint8_t *coeffs;   /* len canonical Fr, 32 B each */
+    size_t len;
+} spx_lc;
+const char *spx_cs_last_error(void);
+int spx_cs_create(spx_cs **out);
+int spx_cs_free(spx_cs *cs);
+int spx_cs_new_input(spx_cs *cs, const uint8_t value[32], uint64_t *var);
+int spx_cs_new_witness(spx_cs *cs, const uint8_t value[32], uint64_t *var);
+int spx_cs_enforce(spx_cs *cs, const spx_lc *a, const spx_lc *b, const spx_lc *c);
+int spx_cs_make_square(spx_cs *cs, uint64_t num_formatted_variables);
+int spx_cs_counts(const spx_cs *cs, uint64_t *constraints, uint64_t *instance, uint64_t *witness);
+int spx_cs_is_satisfied(spx_cs *cs, int *ok);
+int spx_cs_matrices(spx_cs *cs, spx_csr *a, spx_csr *b, spx_csr *c, const uint8_t **v, const uint8_t **w);
+
 /* ---- synthetic instances (SURVEY §8(d) generators; SplitMix64, same draws as the test oracle) ----
  * kind 0 = uniform-3n (satisfiable, nnz = 3n), 1 = ref-shaped (TestSynthesizer, param = density).
  * spx_synth_csr fills views into the handle (valid until spx_synth_free). */

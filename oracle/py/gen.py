@@ -91,7 +91,7 @@ def _row_from_terms(terms):
     return [(acc[c], c) for c in sorted(acc) if acc[c] != 0]
 
 
-def ref_shaped(log_n, log_v=5, density=0, seed=None):
+def ref_shaped(log_n, log_v=5, density=0, seed=None, raw=False):
     n = 1 << log_n
     num_public = 1 << log_v
     num_private = n - num_public
@@ -147,6 +147,7 @@ def ref_shaped(log_n, log_v=5, density=0, seed=None):
         c_val = c_val * c_val % R
         c_var = new_witness(c_val)
         cons.append((lc, list(lc), [(1, c_var)]))
+    raw_cons = [tuple(list(x) for x in k) for k in cons]
     # make_matrices_square: add 0*0 = 0 constraints
     while len(cons) < num_public + num_private:
         cons.append(([], [], []))
@@ -160,6 +161,8 @@ def ref_shaped(log_n, log_v=5, density=0, seed=None):
     B = [_row_from_terms([(c, col(v)) for c, v in b]) for _a, b, _c in cons]
     C = [_row_from_terms([(c, col(v)) for c, v in cc]) for _a, _b, cc in cons]
     assert ninst == num_public and ninst + len(wit_vals) == n
+    if raw:  # the constraints before padding, over ("i", k) / ("w", k) variables (front-end tests)
+        return A, B, C, inst_vals, wit_vals, raw_cons, num_public + num_private
     return A, B, C, inst_vals, wit_vals
 
 

@@ -94,6 +94,15 @@ EXPORTED = [
     "spx_prove_witness",
     "spx_prove_many",
     "spx_last_timings",
+    "spx_cs_create",
+    "spx_cs_free",
+    "spx_cs_new_input",
+    "spx_cs_new_witness",
+    "spx_cs_enforce",
+    "spx_cs_make_square",
+    "spx_cs_counts",
+    "spx_cs_is_satisfied",
+    "spx_cs_matrices",
     "spx_verify",
     "spx_vp_from_pp",
     "spx_pairing_check",
@@ -149,6 +158,15 @@ def lib():
     L.spx_verify.argtypes = [vp, vp, u8p, sz, u8p, sz, u8p, sz, ctypes.POINTER(_Opts)]
     L.spx_vp_from_pp.argtypes = [vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_pairing_check.argtypes = [u8p, u8p, sz, ctypes.POINTER(ctypes.c_int)]
+    L.spx_cs_create.argtypes = [ctypes.POINTER(vp)]
+    L.spx_cs_free.argtypes = [vp]
+    L.spx_cs_new_input.argtypes = [vp, u8p, ctypes.POINTER(ctypes.c_uint64)]
+    L.spx_cs_new_witness.argtypes = [vp, u8p, ctypes.POINTER(ctypes.c_uint64)]
+    L.spx_cs_enforce.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.spx_cs_make_square.argtypes = [vp, ctypes.c_uint64]
+    L.spx_cs_counts.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.spx_cs_is_satisfied.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.spx_cs_matrices.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.spx_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.spx_sum_over_y.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
     L.spx_eval_on_x.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
@@ -429,6 +447,92 @@ class MLArgumentForR1CS:
         _check(lib().spx_verify(pk.ctx.h, pk.h, vb, len(vb) // 32, bytes(proof), len(proof), bytes(vp), len(vp),
                                 ctypes.byref(o)))
         return True
+
+
+class _Lc(ctypes.Structure):
+    _fields_ = [("vars", ctypes.POINTER(ctypes.c_uint64)), ("coeffs", ctypes.c_char_p), ("len", ctypes.c_size_t)]
+
+
+class ConstraintSystem:
+    """R1CS front-end with ark-relations semantics (spx_cs_*): variable ONE = instance 0, inputs
+    numbered before witnesses, compactified rows, make_square as test_utils.rs:81-102."""
+
+    ONE = 0
+
+    def __init__(self):
+        L = lib()
+        L.spx_cs_last_error.restype = ctypes.c_char_p
+        h = ctypes.c_void_p()
+        self._chk(L.spx_cs_create(ctypes.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def _chk(rc):
+        if rc != 0:
+            raise _ERRORS.get(rc, SpartanError)(lib().spx_cs_last_error().decode(errors="replace"))
+
+    def _new(self, fn, value):
+        v = ctypes.c_uint64()
+        self._chk(fn(self.h, (int(value) % R).to_bytes(32, "little"), ctypes.byref(v)))
+        return v.value
+
+    def new_input(self, value):
+        return self._new(lib().spx_cs_new_input, value)
+
+    def new_witness(self, value):
+        return self._new(lib().spx_cs_new_witness, value)
+
+    @staticmethod
+    def _lc(terms):
+        terms = list(terms)
+        vars_ = (ctypes.c_uint64 * max(len(terms), 1))(*[int(v) for _, v in terms])
+        co = b"".join((int(c) % R).to_bytes(32, "little") for c, _ in terms)
+        return _Lc(vars_, co, len(terms)), vars_
+
+    def enforce(self, a, b, c):
+        """a * b == c over lists of (coefficient, variable)."""
+        la, ka = self._lc(a)
+        lb, kb = self._lc(b)
+        lc, kc = self._lc(c)
+        self._chk(lib().spx_cs_enforce(self.h, ctypes.byref(la), ctypes.byref(lb), ctypes.byref(lc)))
+
+    def make_square(self, num_formatted_variables):
+        self._chk(lib().spx_cs_make_square(self.h, int(num_formatted_variables)))
+
+    def counts(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(lib().spx_cs_counts(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def is_satisfied(self):
+        ok = ctypes.c_int()
+        self._chk(lib().spx_cs_is_satisfied(self.h, ctypes.byref(ok)))
+        return ok.value == 1
+
+    def to_matrices(self):
+        """(A, B, C as Csr, v bytes, w bytes) — the inputs of MLArgumentForR1CS.index / prove."""
+        cs = [_CCsr(), _CCsr(), _CCsr()]
+        v, w = ctypes.c_void_p(), ctypes.c_void_p()
+        self._chk(lib().spx_cs_matrices(self.h, *[ctypes.byref(x) for x in cs], ctypes.byref(v), ctypes.byref(w)))
+        ncons, ninst, nwit = self.counts()
+        out = []
+        for x in cs:
+            n = x.n
+            rp = [x.row_ptr[i] for i in range(n + 1)]
+            nnz = rp[-1]
+            col = [x.col[i] for i in range(nnz)]
+            val = ctypes.string_at(x.val, 32 * nnz) if nnz else b""
+            out.append(Csr(n, rp, col, val))
+        vb = ctypes.string_at(v, 32 * ninst)
+        wb = ctypes.string_at(w, 32 * nwit) if nwit else b""
+        return out[0], out[1], out[2], vb, wb
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().spx_cs_free(self.h)
+        except Exception:
+            pass
 
 
 def verifier_parameter(pp):

@@ -83,3 +83,32 @@ def test_verify_oracle_proof(spx, ctx, oc):
     ppc = oc.PP.load(pp.serialize_uncompressed())
     proof = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
     assert spx.MLArgumentForR1CS.verify(pk, inst.v_bytes, proof, vp)
+
+
+def test_frontend_circuit_proves_and_verifies(spx, ctx):
+    """a circuit stated through the R1CS front-end: x^3 + x + 5 = out (the classic example), padded
+    square, proved on the GPU and accepted by the verifier; a wrong witness is rejected."""
+    CS = spx.ConstraintSystem
+    for x_val, ok in ((3, True), (4, False)):
+        cs = CS()
+        out = cs.new_input(35)  # 3^3 + 3 + 5
+        x = cs.new_witness(x_val)
+        x2 = cs.new_witness(x_val * x_val)
+        x3 = cs.new_witness(x_val ** 3)
+        cs.enforce([(1, x)], [(1, x)], [(1, x2)])
+        cs.enforce([(1, x2)], [(1, x)], [(1, x3)])
+        cs.enforce([(1, x3), (1, x), (5, CS.ONE)], [(1, CS.ONE)], [(1, out)])
+        cs.new_input(0)  # |v| = 4 (a power of two: prover.rs:114-116)
+        cs.new_input(0)
+        cs.new_witness(0)  # 8 variables
+        cs.make_square(8)  # 8 constraints (test_utils.rs:81-102)
+        assert cs.is_satisfied() == ok
+        a, b, c, v, w = cs.to_matrices()
+        pk = spx.MLArgumentForR1CS.index(ctx, a, b, c)
+        pp = spx.MLProofForR1CS.setup(ctx, 3, 11)
+        proof = spx.MLArgumentForR1CS.prove(pk, v, w, pp)
+        if ok:
+            assert spx.MLArgumentForR1CS.verify(pk, v, proof, spx.verifier_parameter(pp))
+        else:
+            with pytest.raises((spx.WrongWitness, spx.SumCheckError)):
+                spx.MLArgumentForR1CS.verify(pk, v, proof, spx.verifier_parameter(pp))

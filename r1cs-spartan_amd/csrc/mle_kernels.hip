@@ -334,11 +334,13 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
 __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
                                                          Fr* __restrict__ q, const Fr* __restrict__ point,
                                                          uint64_t half) {
-    const Fr p = ld_fr(point);
+    Fr p{};
+    if (rout) p = ld_fr(point);
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
         fe_sub(d, a1, a0);
         st_fr(q + b, d);
+        if (!rout) continue;  // quotient only (the shared level 0 of the openings)
         fe_mul(t, d, p);
         fe_add(t, a0, t);
         st_fr(rout + b, t);
@@ -426,7 +428,7 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s) {
     kp_begin(KP_OPEN, s);
     hipLaunchKernelGGL(k_open_level, dim3(grid_for(half, 8192)), dim3(kThreads), 0, s, rin, rout, q, point, half);
-    kp_end(32.0 * 4.0 * (double)half, s);  // read 2, write q and r'
+    kp_end(32.0 * (rout ? 4.0 : 3.0) * (double)half, s);  // read 2, write q (and r')
 }
 
 }  // namespace spx

@@ -596,30 +596,70 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
     return commit_finish(C, G);
 }
 
+// ---------------------------------------------------------------- level 0 of both openings
+// open.rs:37-49 at i = 0 reads only the table itself: q_L[b] = z[2b+1] - z[2b] does not depend on
+// the opening point, so pi_0 = MSM(powers_of_h[0], q_L) is the same group element in the opening at
+// (r_v, 0..0) (prover.rs:152) and in the one at r_y (prover.rs:275). It is computed once per proof,
+// launched right behind the commitment (before any challenge exists, overlapping the host's
+// absorption of the matrices) and handed to both open_z calls: a quarter of the proof's G2 work.
+static constexpr size_t kPinLvl0 = 1 << 17;  // pinned offset of the level-0 result (hp uses [0, 64 KiB))
+static bool lvl0_local(int L, int G) { return L - ilog2((uint64_t)G) >= 1; }
+static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank) {
+    const uint64_t half = ((1ull << L) / G) / 2;
+    Fr* q = C.buf<Fr>(Ctx::kSlotLvl0Q, 32 * half);
+    launch_open_level(z_local, nullptr, q, nullptr, half, C.stream);
+    MsmInst I{};
+    I.pts_off = P.g2_off[0] + (uint64_t)rank * half;
+    I.stride = (uint32_t)(1ull << (L - 1));
+    I.scalar_off = 0;
+    I.size = (uint32_t)half;
+    I.c = (uint32_t)P.g2_c[0];
+    I.W = (uint32_t)P.g2_W[0];
+    const size_t xb = 4 * sizeof(Fq2);
+    void* out = C.buf(Ctx::kSlotLvl0Out, xb);
+    msm_run_g2(C.msm, &I, 1, P.g2_pre.as<G2Aff>(), q, out, C.stream);
+    SPX_HIP(hipMemcpyAsync(C.pinned(kPinLvl0 + xb) + kPinLvl0, out, xb, hipMemcpyDeviceToHost, C.stream));
+}
+static Affine<HFq2> lvl0_finish(Ctx& C, int G) {
+    C.sync();
+    Affine<HFq2> part = xyzz_bytes_to_affine<HFq2>(C.pinned(kPinLvl0 + 4 * sizeof(Fq2)) + kPinLvl0);
+    if (G == 1) return part;
+    return sum_affine(allgather_affine(*C.comm, part));
+}
+
 // ---------------------------------------------------------------- open (open.rs:19-58)
 struct OpenOut {
     HFr eval;
     std::vector<Affine<HFq2>> proofs;
 };
-static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector<HFr>& point, int G, int rank) {
+// proof0: the shared level-0 proof (lvl0_launch/lvl0_finish), or null to compute every level here
+static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector<HFr>& point, int G, int rank,
+                      const Affine<HFq2>* proof0 = nullptr) {
     const int g = ilog2((uint64_t)G);
     const uint64_t nl = (1ull << L) / G;
     const int nloc = L - g;  // local levels
+    if (proof0 && nloc < 1) proof0 = nullptr;
+    const int first = proof0 ? 1 : 0;  // first level whose MSM runs here
     OpenOut res;
     res.proofs.resize(L);
+    if (proof0) res.proofs[0] = *proof0;
     Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
     Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * std::max<uint64_t>(nl, 1));
     Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
                    C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
     SPX_HIP(hipMemcpyAsync(pt, point.data(), 32 * L, hipMemcpyHostToDevice, C.stream));  // pageable: staged
-    std::vector<MsmInst> insts(nloc);
+    std::vector<MsmInst> insts(nloc - first);
     const Fr* rin = z_local;
     uint64_t qoff = 0;
     for (int i = 0; i < nloc; ++i) {
         const uint64_t half = nl >> (i + 1);
         Fr* rout = bufs[i & 1];
         launch_open_level(rin, rout, q + qoff, pt + i, half, C.stream);
-        MsmInst& I = insts[i];
+        if (i < first) {  // fold only; the level's proof is proof0 (its quotient is overwritten next)
+            rin = rout;
+            continue;
+        }
+        MsmInst& I = insts[i - first];
         const uint64_t full = 1ull << (L - i - 1);
         I.pts_off = P.g2_off[i] + (uint64_t)rank * half;
         I.stride = (uint32_t)full;
@@ -630,29 +670,30 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
         qoff += half;
         rin = rout;
     }
-    void* out = C.buf(Ctx::kSlotOpenOut, 4 * sizeof(Fq2) * std::max(nloc, 1));
-    msm_run_g2(C.msm, insts.data(), nloc, P.g2_pre.as<G2Aff>(), q, out, C.stream);
+    const int nm = nloc - first;  // MSMs of this batch
+    void* out = C.buf(Ctx::kSlotOpenOut, 4 * sizeof(Fq2) * std::max(nm, 1));
+    msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream);
     const size_t xb = 4 * sizeof(Fq2);
-    uint8_t* h = C.pinned(xb * nloc + 32);
-    SPX_HIP(hipMemcpyAsync(h, out, xb * nloc, hipMemcpyDeviceToHost, C.stream));
-    SPX_HIP(hipMemcpyAsync(h + xb * nloc, rin, 32, hipMemcpyDeviceToHost, C.stream));
+    uint8_t* h = C.pinned(xb * nm + 32);
+    if (nm) SPX_HIP(hipMemcpyAsync(h, out, xb * nm, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(h + xb * nm, rin, 32, hipMemcpyDeviceToHost, C.stream));
     C.sync();
-    std::vector<Affine<HFq2>> part(nloc);
-    for (int i = 0; i < nloc; ++i) part[i] = xyzz_bytes_to_affine<HFq2>(h + xb * i);
-    HFr rlast = ld_hfr(h + xb * nloc);
+    std::vector<Affine<HFq2>> part(nm);
+    for (int k = 0; k < nm; ++k) part[k] = xyzz_bytes_to_affine<HFq2>(h + xb * k);
+    HFr rlast = ld_hfr(h + xb * nm);
     if (G == 1) {
-        res.proofs = part;
+        for (int k = 0; k < nm; ++k) res.proofs[first + k] = part[k];
         res.eval = rlast;
         return res;
     }
     // gather partial proofs and the one remaining local value per rank
-    {
-        std::vector<Affine<HFq2>> all(nloc * G);
-        C.comm->allgather(part.data(), all.data(), sizeof(Affine<HFq2>) * nloc);
-        for (int i = 0; i < nloc; ++i) {
+    if (nm) {
+        std::vector<Affine<HFq2>> all((size_t)nm * G);
+        C.comm->allgather(part.data(), all.data(), sizeof(Affine<HFq2>) * nm);
+        for (int k = 0; k < nm; ++k) {
             std::vector<Affine<HFq2>> v(G);
-            for (int r = 0; r < G; ++r) v[r] = all[r * nloc + i];
-            res.proofs[i] = sum_affine(v);
+            for (int r = 0; r < G; ++r) v[r] = all[(size_t)r * nm + k];
+            res.proofs[first + k] = sum_affine(v);
         }
     }
     std::vector<HFr> rg = allgather_fr(*C.comm, {rlast});  // global r_g table (G entries)
@@ -779,6 +820,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     }
     // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
     commit_launch(C, P, z, n, G, rank);
+    const bool share0 = lvl0_local(L, G);
+    if (share0) lvl0_launch(C, P, zl, L, G, rank);
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
@@ -806,6 +849,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     }
     mark("transcript_matrices", tp);
     Affine<HFq> com = commit_finish(C, G);
+    Affine<HFq2> proof0{};
+    if (share0) proof0 = lvl0_finish(C, G);
     Ser proof;
     {
         size_t m0 = proof.b.size();
@@ -820,7 +865,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = open_z(C, P, zl, L, pt1, G, rank);
+        OpenOut op = open_z(C, P, zl, L, pt1, G, rank, share0 ? &proof0 : nullptr);
         size_t m0 = proof.b.size();
         ser_open(proof, op.eval, P, op.proofs);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
@@ -1047,7 +1092,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     mark("sumcheck2", tp);
     // ---- round 6: open at r_y (prover.rs:268-281)
     {
-        OpenOut op = open_z(C, P, zl, L, r_y, G, rank);
+        OpenOut op = open_z(C, P, zl, L, r_y, G, rank, share0 ? &proof0 : nullptr);
         ser_open(proof, op.eval, P, op.proofs);
     }
     mark("open_ry", tp);

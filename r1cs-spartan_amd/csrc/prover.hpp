@@ -124,7 +124,7 @@ struct Ctx {
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
-    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotTailQ, kSlotTailOut, kSlots };
+    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotTailQ, kSlotTailOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
     DevMem slot[kSlots];
     template <class T = void>
     T* buf(int id, size_t bytes) {

@@ -302,12 +302,14 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
                 set_dev(ctxs[k]);
                 spx::ProveOpts o = base;
                 o.seq = i;
-                if (!base.cached && i % G == rank) {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return slots[i].state.load() != 0; });
-                    if (slots[i].state.load() == 2) throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
-                    o.absorbed = &slots[i].h;
-                }
+                if (!base.cached && i % G == rank)  // waited for inside prove, behind the proof's first kernels
+                    o.await_absorbed = [&, i]() -> const spx::Blake2s* {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return slots[i].state.load() != 0; });
+                        if (slots[i].state.load() == 2)
+                            throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
+                        return &slots[i].h;
+                    };
                 auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, *pp->p, o);
                 if (p.size() > stride) spx::invalid("proof buffer too small");
                 memcpy(out + (size_t)i * stride, p.data(), p.size());

@@ -125,8 +125,7 @@ struct MsmInst {
     uint32_t size;        // number of (base, scalar) pairs
     uint32_t c, W;        // window bits, windows
     uint32_t bucket_off;  // first bucket of this instance (2^(c-1) buckets)
-    uint32_t red_off;     // first bucket-reduction slot
-    uint32_t red_T, red_L;  // reduction threads and buckets per thread
+    uint32_t ref_off;     // first (bucket, reference) slot of this instance (radix-sort layout)
     uint32_t stride;      // points per window copy of the base set (>= size; local blocks)
 };
 

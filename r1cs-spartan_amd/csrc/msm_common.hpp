@@ -78,7 +78,7 @@ struct DBuf {
 
 struct MsmWorkspace {
     DBuf insts, prefix, redp, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, maxv,
-        tprefix;
+        tprefix, keys_a, keys_b, vals_a;
     uint32_t* h_max = nullptr;
     MsmWorkspace() { HIPCHK(hipHostMalloc((void**)&h_max, sizeof(uint32_t))); }
     ~MsmWorkspace() {
@@ -98,6 +98,9 @@ struct MsmSorted {
     std::vector<MsmInst> insts;  // host copy with bucket offsets filled in
 };
 MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s);
+// partials of the load-balanced affine level per bucket: the seg-length thread ranges its references meet
+void launch_partial_counts(const uint32_t* off, const uint32_t* cnt, uint32_t nb, uint32_t* np, uint32_t seg,
+                           hipStream_t s);
 void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s);
 
 }  // namespace spx

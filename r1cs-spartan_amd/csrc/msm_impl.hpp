@@ -9,23 +9,37 @@ namespace spx {
 // ------------------------------------------------------------------ accumulation levels
 // Accumulation and weighting run in the radix-2^29 domain (ff29.hpp / curve29.hpp): tables and
 // partials in memory hold R = 2^406 Montgomery values (< 2p), packed into the 12-word layout.
+// Load-balanced: thread t adds references [t seg1, (t+1) seg1) of the bucket-sorted array whatever
+// the bucket boundaries, so every lane runs the same number of additions. A thread whose range
+// crosses into the next (non-empty) bucket stores the finished partial and restarts; bucket b's
+// partials are pfx[b] + (t - off[b] / seg1) for the threads t its range intersects.
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict__ segoff, uint32_t nb,
-                                                      const uint32_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ cnt,
+__global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict__ off, uint32_t nb,
+                                                      const uint32_t* __restrict__ pfx,
                                                       const uint32_t* __restrict__ refs,
                                                       const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out,
                                                       uint32_t seg1) {
     using T = typename R29<F>::T;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= segoff[nb]) return;
-    const uint32_t b = find_bucket(segoff, nb, s);
-    const uint32_t k = s - segoff[b];
-    const uint32_t start = off[b] + k * seg1;
-    const uint32_t end = min(start + seg1, off[b] + cnt[b]);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t total = off[nb];
+    uint32_t e = t * seg1;
+    if (e >= total) return;
+    const uint32_t end = min(e + seg1, total);
+    uint32_t b = find_bucket(off, nb, e);
+    uint32_t bend = off[b + 1];
+    uint32_t slot = pfx[b] + (t - off[b] / seg1);
     X29<T> acc;
     x29_set_inf(acc);
-    for (uint32_t e = start; e < end; ++e) {
+    for (; e < end; ++e) {
+        if (e == bend) {  // bucket b is finished inside this range: the next one starts here
+            st29<F>(out + slot, acc);
+            x29_set_inf(acc);
+            do {
+                ++b;
+            } while (off[b + 1] <= e);  // skip empty buckets
+            bend = off[b + 1];
+            slot = pfx[b];
+        }
         const uint32_t r = refs[e];
         Aff<F> p;
         load_vec(p, pts + (r & 0x7fffffffu));
@@ -35,7 +49,7 @@ __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict
         R29<F>::unpack(py, p.y);
         x29_madd(acc, px, py, (r >> 31) != 0);
     }
-    st29<F>(out + s, acc);
+    st29<F>(out + slot, acc);
 }
 
 template <class F>
@@ -182,11 +196,12 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
-    launch_seg_counts(so.counts, nb, so.segcnt, kSeg1, s);
+    launch_partial_counts(so.offs, so.counts, nb, so.segcnt, kSeg1, s);
     exclusive_scan(ws, so.segcnt, so.soa, nb + 1, s);
+    const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
-    hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((max_segs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.soa,
-                       nb, so.offs, so.counts, so.refs, pts, PA, kSeg1);
+    hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((nthr + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.offs, nb,
+                       so.soa, so.refs, pts, PA, kSeg1);
     // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
     kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s, (double)tot_refs);
     uint32_t* cur_cnt = so.segcnt;
@@ -196,7 +211,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     Xyzz<F>* cur = PA;
     Xyzz<F>* nxt = PB;
     uint64_t cur_max_segs = max_segs;
-    uint32_t m = (so.maxc + kSeg1 - 1) / kSeg1;
+    uint32_t m = so.maxc ? (so.maxc + kSeg1 - 1) / kSeg1 + 1 : 1;  // partials per bucket (a range may straddle)
     while (m > 1) {
         launch_seg_counts(cur_cnt, nb, spare_cnt, kSeg, s);
         exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);

@@ -825,17 +825,18 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
+    const Blake2s* absorbed = o.await_absorbed ? o.await_absorbed() : o.absorbed;
     if (o.cached && I.has_cache)
         T.set_state(I.cache);
     else if (G == 1) {
-        T.set_state(o.absorbed ? *o.absorbed : absorb_matrices(I));
+        T.set_state(absorbed ? *absorbed : absorb_matrices(I));
     } else {
         // the (sequential, ~150 MB at 2^20) absorption of A, B, C is done once per proof, by one rank
         // in turn; the others take its Blake2s state from the allgather (bit-identical transcript)
         static_assert(std::is_trivially_copyable<Blake2s>::value, "Blake2s state is shipped as bytes");
         const int owner = (int)(seq % (uint64_t)G);
         Blake2s h;
-        if (rank == owner) h = o.absorbed ? *o.absorbed : absorb_matrices(I);
+        if (rank == owner) h = absorbed ? *absorbed : absorb_matrices(I);
         std::vector<uint8_t> all(sizeof(Blake2s) * G);
         comm.allgather(&h, all.data(), sizeof(Blake2s));
         memcpy(&h, all.data() + sizeof(Blake2s) * owner, sizeof(Blake2s));

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -210,6 +211,9 @@ struct ProveOpts {
     // scheduling hooks used by spx_prove_many (neither changes the proof):
     int64_t seq = -1;                 // proof number deciding which rank absorbs A, B, C (default: ctx counter)
     const Blake2s* absorbed = nullptr;  // this proof's A, B, C absorption, already computed by the caller
+    // or, when set, called once the challenge-independent device work (SpMV, commitment MSM, shared
+    // level-0 opening MSM) is queued, and returns that absorption (waiting for it if needed)
+    std::function<const Blake2s*()> await_absorbed;
 };
 // Blake2s state after absorbing A, B, C (lib.rs:61-64): the per-proof sequential host work
 Blake2s absorb_matrices(const Index& I);

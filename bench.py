@@ -8,10 +8,11 @@ proof), G1 commit MSM, two mKZG openings (G2 MSMs), SpMVs, eq tables, both sumch
 serialization. Setup (keygen), index and witness upload are outside the timed region, as in
 benchmark.rs:26-35.
 
-One step = a batch of --inflight proofs; the K timed steps run as one continuous pipeline of K x B
-proofs through spx_prove_many (B host worker threads, each with its own HIP stream and MSM
-workspace, each proving its share back to back), so the sequential host Blake2s absorption of the
-matrices (~150 MB per proof) overlaps other proofs' GPU work instead of idling the GPU.
+One step = a batch of P = --proofs-per-step proofs (default 64); the K timed steps run as one
+continuous pipeline of K x P proofs through spx_prove_many with B = --inflight (default 16) host
+worker threads, each with its own HIP stream and MSM workspace, each proving its share back to
+back, so the sequential host Blake2s absorption of the matrices (~150 MB per proof, one pool of
+hashing threads per rank) overlaps other proofs' GPU work instead of idling the GPU.
 value = constraints proved per second over the timed region (whole job). The single-proof latency
 and the index-cached-transcript variant are reported beside it.
 
@@ -143,9 +144,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--shard", default="batch", choices=["batch", "proof"],
+                    help="N > 1 headline: 'batch' = every rank proves its own proofs (weak scaling, no data-path "
+                    "exchange); 'proof' = every proof split over all ranks (strong scaling, per-round exchange)")
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="N > 1 with --shard batch: skip the secondary proof-sharded measurement")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
                     help="N > 1 transport: on-node shared memory (default) or RCCL AllGather")
-    ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts) = proofs per step")
+    ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts)")
+    ap.add_argument("--proofs-per-step", type=int, default=64,
+                    help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,20 +184,27 @@ def main():
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     spx = load_product()
     B = max(1, args.inflight)
+    P = max(B, (args.proofs_per_step + B - 1) // B * B)  # proofs per step; each worker proves P / B of them
     # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
     device = 0 if os.environ.get("SPX_BENCH_SAME_GPU") == "1" else local
+    sharded_head = world > 1 and args.shard == "proof"
+    # batch mode (and N = 1): contexts with the local communicator, every rank proves whole proofs
     ctxs = [spx.Context(device) for _ in range(B)]
     ctx = ctxs[0]
-    if world > 1 and args.comm == "rccl":
-        uid = [[spx.comm_unique_id() for _ in range(B)] if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        for k, c in enumerate(ctxs):
-            c.set_comm_rccl(uid[0][k], rank, world)
-    elif world > 1:
-        name = [spx.shm_name() if rank == 0 else None]
-        dist.broadcast_object_list(name, src=0)
-        for k, c in enumerate(ctxs):
-            c.set_comm_shm("%s_%d" % (name[0], k), rank, world)
+    # proof-sharded contexts (N > 1): one communicator per proof in flight, every proof split over the ranks
+    sctxs = []
+    if world > 1 and (sharded_head or not args.no_sharded):
+        sctxs = [spx.Context(device) for _ in range(B)]
+        if args.comm == "rccl":
+            uid = [[spx.comm_unique_id() for _ in range(B)] if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            for k, c in enumerate(sctxs):
+                c.set_comm_rccl(uid[0][k], rank, world)
+        else:
+            name = [spx.shm_name() if rank == 0 else None]
+            dist.broadcast_object_list(name, src=0)
+            for k, c in enumerate(sctxs):
+                c.set_comm_shm("%s_%d" % (name[0], k), rank, world)
 
     log_n, log_v = args.log_n, args.log_v
     n = 1 << log_n
@@ -200,20 +215,14 @@ def main():
     pp = spx.MLProofForR1CS.setup(ctx, log_n, 0xC0FFEE)
     t_setup = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pkh = index_from_c(spx, ctx, mats)
-    pk = spx.IndexPK(ctx, pkh, log_n)
+    pk = spx.IndexPK(ctx, index_from_c(spx, ctx, mats), log_n)
+    spk = spx.IndexPK(sctxs[0], index_from_c(spx, sctxs[0], mats), log_n) if sctxs else None
     wit = spx.Witness(ctx, z[: 32 << log_v], z[32 << log_v :])
     t_index = time.perf_counter() - t0
 
     def barrier():
         if dist is not None:
             dist.barrier()
-
-    def prove(cached=False):
-        return spx.MLArgumentForR1CS.prove_witness(pk, wit, pp, mode=args.mode, seed=7, cached=cached)
-
-    def prove_batch(steps, cached=False):
-        return spx.MLArgumentForR1CS.prove_many(ctxs, pk, [wit] * (B * steps), pp, mode=args.mode, seed=7, cached=cached)
 
     def timed(fn):
         barrier()
@@ -222,47 +231,70 @@ def main():
         barrier()
         return r, time.perf_counter() - t0
 
-    proofs = prove_batch(max(1, args.warmup))
+    def batch_fn(cs, k, steps, cached=False):
+        return lambda: spx.MLArgumentForR1CS.prove_many(cs, k, [wit] * (P * steps), pp, mode=args.mode, seed=7,
+                                                        cached=cached)
+
+    def single_fn(k):
+        def run():
+            for _ in range(args.steps):
+                r = spx.MLArgumentForR1CS.prove_witness(k, wit, pp, mode=args.mode, seed=7)
+            return r
+        return run
+
+    # headline configuration
+    hctxs, hpk = (sctxs, spk) if sharded_head else (ctxs, pk)
+    hctx = hctxs[0]
+    batch_fn(hctxs, hpk, max(1, args.warmup))()
     L = spx.lib()
     if not args.no_stats:
-        spx._check(L.spx_kernel_stats_enable(ctx.h, 1))
-    # ---- timed region (headline): K steps x B full proofs, pipelined over B workers
-    proofs, elapsed = timed(lambda: prove_batch(args.steps))
+        spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
+    # ---- timed region (headline): K steps x P full proofs, pipelined over B workers
+    proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps))
     stats = {}
     if not args.no_stats:
         for k, name in enumerate(KNAMES):
             cnt, kms, by, ops = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-            spx._check(L.spx_kernel_stats(ctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
-            spx._check(L.spx_kernel_ops(ctx.h, k, ctypes.byref(ops)))
+            spx._check(L.spx_kernel_stats(hctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
+            spx._check(L.spx_kernel_ops(hctx.h, k, ctypes.byref(ops)))
             if cnt.value:
-                # ctx 0 proves one proof per step
-                stats[name] = {"launches": cnt.value / args.steps, "ms": kms.value / args.steps,
-                               "bytes": by.value / args.steps, "ops": ops.value / args.steps}
-        spx._check(L.spx_kernel_stats_enable(ctx.h, 0))
+                # per proof: ctx 0 proves P / B proofs per step
+                per = args.steps * (P // B)
+                stats[name] = {"launches": cnt.value / per, "ms": kms.value / per, "bytes": by.value / per,
+                               "ops": ops.value / per}
+        spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
     assert all(p == proofs[0] for p in proofs), "concurrent proofs differ"
     proof = proofs[0]
     # ---- single-proof latency (one proof at a time) and its phase split
-    def single():
-        for _ in range(args.steps):
-            r = prove()
-        return r
-
-    p1, elapsed_single = timed(single)
+    p1, elapsed_single = timed(single_fn(hpk))
     assert p1 == proof, "single proof differs from the batched one"
-    phases = ctx.last_timings()
+    phases = hctx.last_timings()
     # ---- index-cached transcript variant (matrix absorption moved to index time; bit-identical)
-    p2, elapsed_cached = timed(lambda: prove_batch(args.steps, cached=True))
+    p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True))
     assert all(p == proof for p in p2), "cached-transcript proof differs"
+    # ---- N > 1, batch headline: the same proofs split over all ranks (throughput and latency)
+    ms_s = ms_s1 = None
+    if sctxs and not sharded_head:
+        batch_fn(sctxs, spk, 1)()
+        p3, el = timed(batch_fn(sctxs, spk, args.steps))
+        assert all(p == proof for p in p3), "proof-sharded proof differs"
+        p4, el1 = timed(single_fn(spk))
+        assert p4 == proof, "proof-sharded single proof differs"
+        ms_s, ms_s1 = el / args.steps * 1e3, el1 / args.steps * 1e3
 
-    ms = elapsed / args.steps * 1e3  # per step (B proofs)
+    ms = elapsed / args.steps * 1e3  # per step (P proofs)
     ms_c = elapsed_cached / args.steps * 1e3
     ms_1 = elapsed_single / args.steps * 1e3
     if dist is not None:
         import torch
 
-        t = torch.tensor([ms, ms_c, ms_1], dtype=torch.float64)
+        t = torch.tensor([ms, ms_c, ms_1, ms_s or 0.0, ms_s1 or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms, ms_c, ms_1 = float(t[0]), float(t[1]), float(t[2])
+        if ms_s is not None:
+            ms_s, ms_s1 = float(t[3]), float(t[4])
+    # whole-job throughput: in batch mode every rank proves P proofs per step, sharded all ranks share them
+    jobs = P * (1 if sharded_head else world)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -270,7 +302,10 @@ def main():
 
     roof = None
     if stats:
-        dom = max(stats, key=lambda k: stats[k]["ms"])
+        # dominant kernel = largest share of a proof's GPU time when it runs alone (rocprofv3, one proof
+        # in flight: profiles/*kernel_stats_inflight1*.csv). Live durations under P proofs in flight
+        # overlap, so the latency-bound weighting-tree launches would otherwise look longest.
+        dom = "msm_acc_g2" if "msm_acc_g2" in stats else max(stats, key=lambda k: stats[k]["ms"])
         d = stats[dom]
         avg_s = d["ms"] / d["launches"] / 1e3
         per_launch = d["bytes"] / d["launches"]
@@ -298,37 +333,38 @@ def main():
                 "achieved_per_launch": round(d["ops"] / d["launches"] / avg_s, 1),
                 "frac_per_launch": round(d["ops"] / d["launches"] / avg_s / MADD_CEILING[dom], 4),
                 # whole job: this kernel's additions of every proof in the timed region / wall time
-                "achieved_job": round(per_proof_ops * B / (ms / 1e3), 1),
-                "frac_job": round(per_proof_ops * B / (ms / 1e3) / MADD_CEILING[dom], 4),
+                "achieved_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3), 1),
+                "frac_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3) / MADD_CEILING[dom], 4),
             }
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds)
     out = {
         "metric": "R1CS constraints proved/sec at 2^%d" % log_n,
-        "value": round(B * n / (ms / 1e3), 1),
+        "value": round(jobs * n / (ms / 1e3), 1),
         "unit": "constraints/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if sharded_head else "weak",
         "vs_baseline": None,
         "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
         "data": "synthetic",
         "config": {
             "workload": "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, full prove + commit + 2 openings, %s transcript, "
-            "%d proofs in flight per step" % ("uniform-3n" if args.kind == 0 else "ref-shaped", log_n, 1 << log_v, nnz,
-                                              args.mode.upper(), B),
+            "%d proofs per step, %d in flight" % ("uniform-3n" if args.kind == 0 else "ref-shaped", log_n, 1 << log_v,
+                                                   nnz, args.mode.upper(), P, B),
             "log_n": log_n,
-            "proofs_per_step": B,
-            "parallelism": "shard%d" % world,
-            "comm": args.comm if world > 1 else None,
+            "proofs_per_step": P,
+            "proofs_in_flight": B,
+            "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
+            "comm": args.comm if sctxs else None,
         },
         "ms_per_proof_single": round(ms_1, 3),
         "value_single_proof": round(n / (ms_1 / 1e3), 1),
-        "value_index_cached_transcript": round(B * n / (ms_c / 1e3), 1),
+        "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1),
         "ms_per_step_index_cached_transcript": round(ms_c, 3),
         "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
         "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in stats.items()},
@@ -339,6 +375,11 @@ def main():
         "gen_s": round(t_gen, 2),
         "proof_bytes": len(proof),
     }
+    if ms_s is not None:
+        # the same workload with every proof split over all ranks (hypercube blocks, per-round exchange)
+        out["value_proof_sharded"] = round(P * n / (ms_s / 1e3), 1)
+        out["ms_per_step_proof_sharded"] = round(ms_s, 3)
+        out["ms_per_proof_single_proof_sharded"] = round(ms_s1, 3)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

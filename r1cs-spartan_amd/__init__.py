@@ -22,7 +22,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspartan_hip.so")
+LIB_PATH = os.environ.get("SPX_LIB_PATH") or os.path.join(_HERE, "libspartan_hip.so")  # override: A/B builds
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 

@@ -40,6 +40,8 @@ __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict
             bend = off[b + 1];
             slot = pfx[b];
         }
+        // (a software-pipelined variant that issues the next point's load before this addition
+        // measured 2.5% slower end to end: more AGPR traffic at occupancy 1)
         const uint32_t r = refs[e];
         Aff<F> p;
         load_vec(p, pts + (r & 0x7fffffffu));

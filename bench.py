@@ -40,8 +40,8 @@ MADD_CEILING = {"msm_acc_g2": 1.96e9, "msm_acc_g1": 5.78e9}
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
 KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
-        "open_level": "k_open_level", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq>",
-        "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq>", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
+        "open_level": "k_open_level", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
+        "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq >", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 

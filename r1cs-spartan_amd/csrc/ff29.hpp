@@ -67,55 +67,74 @@ DEV void f29_zero(F29& r) {
 }
 DEV void f29_one(F29& r) { f29_set(r, Q29::ONE); }
 
-// r = REDC(a b) = a b / 2^406 mod p, < 2p for inputs < 2^392
-DEV void f29_mul(F29& r, const F29& a, const F29& b) {
+// Each Montgomery column is summed in SPX_F29_CHAINS independent 64-bit chains (products dealt
+// round-robin, the m[k-1] p[1] product last), joined with the previous column's carry at the end:
+// the column's products do not wait for the previous column, and the dependent chain per
+// coefficient is short enough to hide the v_mad_u64_u32 latency at one wave per SIMD.
+#ifndef SPX_F29_CHAINS
+#define SPX_F29_CHAINS 1
+#endif
+
+template <int NC>
+DEV uint64_t f29_join(const uint64_t (&ch)[NC], uint64_t carry) {
+    if constexpr (NC == 1) return ch[0] + carry;
+    else if constexpr (NC == 2) return (ch[0] + ch[1]) + carry;
+    else if constexpr (NC == 3) return (ch[0] + ch[1]) + (ch[2] + carry);
+    else return ((ch[0] + ch[1]) + (ch[2] + ch[3])) + carry;
+}
+
+// REDC(sum of NP products a_j b_j): NP = 1 (f29_mul) or 2 (f29_mul2, lazy reduction)
+template <int NP>
+DEV void f29_redc_sum(F29& r, const F29* const (&a)[NP], const F29* const (&b)[NP]) {
+    constexpr int NC = SPX_F29_CHAINS;
     uint32_t m[14], t[14];
-    uint64_t acc = 0;
+    uint64_t carry = 0;
 #pragma unroll
     for (int k = 0; k < 27; ++k) {
         const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+        uint64_t ch[NC];
 #pragma unroll
-        for (int i = lo; i <= hi; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+        for (int c = 0; c < NC; ++c) ch[c] = 0;
+        int j = 0;
 #pragma unroll
-        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) acc += (uint64_t)m[i] * Q29::P[k - i];
+        for (int i = lo; i <= hi; ++i) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                ch[j % NC] += (uint64_t)a[q]->v[i] * b[q]->v[k - i];
+                ++j;
+            }
+        }
+#pragma unroll
+        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) {
+            ch[j % NC] += (uint64_t)m[i] * Q29::P[k - i];
+            ++j;
+        }
+        uint64_t acc = f29_join<NC>(ch, carry);
         if (k < 14) {
             m[k] = ((uint32_t)acc * Q29::PINV) & Q29::M;
             acc += (uint64_t)m[k] * Q29::P[0];
         } else {
             t[k - 14] = (uint32_t)acc & Q29::M;
         }
-        acc >>= 29;
+        carry = acc >> 29;
     }
-    t[13] = (uint32_t)acc;
+    t[13] = (uint32_t)carry;
 #pragma unroll
     for (int i = 0; i < 14; ++i) r.v[i] = t[i];
 }
 
+// r = REDC(a b) = a b / 2^406 mod p, < 2p for inputs < 2^392
+DEV void f29_mul(F29& r, const F29& a, const F29& b) {
+    const F29* const pa[1] = {&a};
+    const F29* const pb[1] = {&b};
+    f29_redc_sum<1>(r, pa, pb);
+}
+
 // r = REDC(a b + c d): one reduction for a sum of two products (lazy reduction)
 DEV void f29_mul2(F29& r, const F29& a, const F29& b, const F29& c, const F29& d) {
-    uint32_t m[14], t[14];
-    uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 27; ++k) {
-        const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
-#pragma unroll
-        for (int i = lo; i <= hi; ++i) {
-            acc += (uint64_t)a.v[i] * b.v[k - i];
-            acc += (uint64_t)c.v[i] * d.v[k - i];
-        }
-#pragma unroll
-        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) acc += (uint64_t)m[i] * Q29::P[k - i];
-        if (k < 14) {
-            m[k] = ((uint32_t)acc * Q29::PINV) & Q29::M;
-            acc += (uint64_t)m[k] * Q29::P[0];
-        } else {
-            t[k - 14] = (uint32_t)acc & Q29::M;
-        }
-        acc >>= 29;
-    }
-    t[13] = (uint32_t)acc;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) r.v[i] = t[i];
+    const F29* const pa[2] = {&a, &c};
+    const F29* const pb[2] = {&b, &d};
+    f29_redc_sum<2>(r, pa, pb);
 }
 
 DEV void f29_add(F29& r, const F29& a, const F29& b) {

@@ -14,6 +14,7 @@ namespace spx {
 static constexpr uint32_t kSeg1Default = 32;  // references per thread, affine accumulation level
 uint32_t seg1_len(bool g2);                      // kSeg1Default unless SPX_KSEG1 / SPX_KSEG1_G2 (tuning)
 static constexpr uint32_t kSeg = 32;    // partials per thread, XYZZ accumulation levels
+static constexpr uint32_t kTreeChunkLog = 4;  // buckets per running-sum chunk of the weighting leaf: 16
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
 

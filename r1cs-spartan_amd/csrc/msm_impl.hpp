@@ -76,52 +76,70 @@ __global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restric
     st29<F>(out + s, acc);
 }
 
-// ------------------------------------------------------------------ bucket weighting: low-depth tree
-// Result = sum_j (j+1) S_j over the B = 2^(c-1) bucket sums of an instance. Binary tree over the
-// buckets; node = (F, S, D) with F = sum_m (m+1) X_m (local index m), S = sum X_m, D = size * S:
+// ------------------------------------------------------------------ bucket weighting: chunks + tree
+// Result = sum_j (j+1) S_j over the B = 2^(c-1) bucket sums of an instance. Node = (F, S, D) over a
+// run of consecutive buckets, with F = sum_m (m+1) X_m (local index m), S = sum X_m, D = size * S.
+// Leaf level, chunked (k_tree_chunk): one thread sums m = 2^lgm consecutive buckets by a running
+// sum (from the top bucket down: run += X_j, F += run), giving the chunk's node (F, S, D = m S) in
+// 2m additions + lgm doublings (a pairwise tree spends ~5 group operations per bucket on the
+// levels this replaces). Above it, a binary tree over the chunks:
 //   parent(l, r) = (F_l + D_r + F_r,  S_l + S_r,  2 (D_l + D_r))      (size(l) = size(r))
-// One level per launch, one thread per (node, component), component-major so every wave runs one
-// component (no divergence between the F / S / D formulas): the dependent depth is 2 group
-// operations per level (~2 log2 B in total) instead of a per-thread running sum over many
-// buckets — single-lane latency of a G2 addition is ~100 us on CDNA4, so depth is what matters.
-// A missing right child (instances with fewer buckets) is the point at infinity: F and S pass
+// one level per launch, one thread per (node, component), component-major so every wave runs one
+// component (no divergence between the F / S / D formulas): 2 group operations of dependent
+// depth per level (single-lane latency of a G2 addition is ~45 us on CDNA4).
+// A missing right child (instances with fewer chunks) is the point at infinity: F and S pass
 // through unchanged, so all instances of a batch run the same number of levels.
-template <class F>
-DEV void ld_bucket(X29<typename R29<F>::T>& x, uint32_t b, const uint32_t* cnt, const uint32_t* off,
-                   const Xyzz<F>* P) {
-    if (cnt[b])
-        ld29<F>(x, P + off[b]);
-    else
-        x29_set_inf(x);
-}
+DEV uint32_t tree_chunk_log(uint32_t c) { return c - 2 < kTreeChunkLog ? c - 2 : kTreeChunkLog; }
 
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_tree_leaf(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp,
-                                                      int ninst, const uint32_t* __restrict__ node_off,
-                                                      const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                                      const Xyzz<F>* __restrict__ P, Xyzz<F>* __restrict__ Fo,
-                                                      Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
+__global__ __launch_bounds__(kHeavy) void k_tree_chunk(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp,
+                                                       int ninst, const uint32_t* __restrict__ node_off,
+                                                       const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                                                       const Xyzz<F>* __restrict__ P, Xyzz<F>* __restrict__ Fo,
+                                                       Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
     const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    const uint64_t N = wp[ninst];  // output nodes; component-major so a wave runs one component
-    if (t >= 3 * N) return;
-    const uint32_t comp = (uint32_t)(t / N);
-    const uint64_t tn = t - comp * N;
-    const int i = find_slot(wp, ninst, tn);
-    const uint32_t k = (uint32_t)(tn - wp[i]);
+    if (t >= wp[ninst]) return;
+    const int i = find_slot(wp, ninst, t);
+    const uint32_t k = (uint32_t)(t - wp[i]);
     const MsmInst I = insts[i];
-    X29<typename R29<F>::T> l, r;
-    ld_bucket(l, I.bucket_off + 2 * k, cnt, off, P);
-    ld_bucket(r, I.bucket_off + 2 * k + 1, cnt, off, P);
+    const uint32_t lgm = tree_chunk_log(I.c);
+    const uint32_t b0 = I.bucket_off + (k << lgm);
     const uint32_t o = node_off[i] + k;
-    if (comp == 0) {  // F = X_l + 2 X_r
-        x29_dbl(r);
-        x29_add(r, l);
-        st29<F>(Fo + o, r);
-    } else {
-        x29_add(l, r);
-        if (comp == 2) x29_dbl(l);
-        st29<F>((comp == 1 ? So : Do) + o, l);
+    // F accumulates in its output slot, and both kinds of step (run += X_j, F += run) go through one
+    // addition site with two points live: a G2 XYZZ point is 112 registers in radix 2^29
+    using T = typename R29<F>::T;
+    X29<T> run;
+    x29_set_inf(run);
+    const int m = 1 << lgm;
+#pragma unroll 1
+    for (int st = 0; st < 2 * m; ++st) {
+        const int j = m - 1 - (st >> 1);
+        const bool bucket_step = (st & 1) == 0;
+        X29<T> a, b;
+        if (bucket_step) {
+            if (!cnt[b0 + j]) continue;
+            a = run;
+            ld29<F>(b, P + off[b0 + j]);
+        } else {
+            if (j == m - 1) {  // F = run for the top bucket
+                st29<F>(Fo + o, run);
+                continue;
+            }
+            ld29<F>(a, Fo + o);
+            b = run;
+        }
+        x29_add(a, b);
+        if (bucket_step) {
+            run = a;
+        } else {
+            st29<F>(Fo + o, a);
+            run = b;
+        }
     }
+    st29<F>(So + o, run);
+#pragma unroll 1
+    for (uint32_t d = 0; d < lgm; ++d) x29_dbl(run);
+    st29<F>(Do + o, run);
 }
 
 template <class F>
@@ -234,9 +252,11 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     int levels = 0;
     for (int i = 0; i < ninst; ++i) {
         node_off[i] = tot_nodes;
-        cnt[i] = 1u << (so.insts[i].c - 2);  // nodes after the leaf level (B / 2; c >= 3)
+        // nodes after the chunked leaf level: B / 2^lgm (c >= 3, lgm = min(kTreeChunkLog, c - 2))
+        const int lg = (int)so.insts[i].c - 1 - (int)std::min<uint32_t>(kTreeChunkLog, so.insts[i].c - 2);
+        cnt[i] = 1u << lg;
         tot_nodes += cnt[i];
-        levels = std::max(levels, (int)so.insts[i].c - 2);
+        levels = std::max(levels, lg);
     }
     // per-level work prefixes: 3 threads per output node; per-level input node counts
     std::vector<uint64_t> wp((size_t)(levels + 1) * (ninst + 1));
@@ -266,8 +286,8 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     Xyzz<F>* B3[3] = {TB, TB + tot_nodes, TB + 2 * (size_t)tot_nodes};
     kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     {
-        uint64_t work = 3 * wp[ninst];
-        hipLaunchKernelGGL(k_tree_leaf<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
+        uint64_t work = wp[ninst];
+        hipLaunchKernelGGL(k_tree_chunk<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
                            so.d_insts, d_wp, ninst, d_noff, cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
     }
     for (int lv = 1; lv <= levels; ++lv) {

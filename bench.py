@@ -45,6 +45,25 @@ KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_spar
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
+VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
+
+
+def valu_issue(ms_per_proof, dom):
+    """Compute-side roofline of the whole proof: the VALU wave-instructions every proof kernel issues
+    (rocprofv3 SQ_INSTS_VALU pass, tools/valu_summary.py -> profiles/pmc_valu.json) at the full issue
+    rate (4 cycles per wave-instruction on each of the 1024 SIMDs), against the measured time per proof."""
+    try:
+        d = json.load(open(VALU_FILE))
+    except (OSError, ValueError):
+        return None
+    ideal = d["ideal_valu_ms_per_proof"]
+    k = d["kernels"].get(KSYM.get(dom, ""), {})
+    return {"ideal_ms_per_proof": round(ideal, 3), "ms_per_proof": round(ms_per_proof, 3),
+            "frac": round(ideal / ms_per_proof, 4),
+            "dominant_kernel_ideal_ms_per_proof": round(k.get("ideal_valu_ms_per_proof", 0.0), 3),
+            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU, %g proofs, %g GHz)" % (d["proofs"], d["clock_ghz"])}
+
+
 def pmc_traffic(kname):
     """HBM bytes per launch of `kname` from the committed rocprofv3 PMC passes (tools/pmc_summary.py)."""
     try:
@@ -60,6 +79,11 @@ def pmc_traffic(kname):
 
 KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
           "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]
+
+
+def jobs_per_rank_step(P, world, sharded_head):
+    """proofs one rank's GPU completes per step: P in batch mode; P / world of each proof's work sharded"""
+    return P if not sharded_head else P / world * 1.0
 
 
 def load_product():
@@ -336,6 +360,10 @@ def main():
                 "achieved_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3), 1),
                 "frac_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3) / MADD_CEILING[dom], 4),
             }
+    if roof is not None:
+        vi = valu_issue(ms / jobs_per_rank_step(P, world, sharded_head), roof["kernel"])
+        if vi:
+            roof["valu_issue"] = vi
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds)

@@ -132,6 +132,10 @@ DEV void x29_dbl(X29<F>& p) {
 }
 
 // p += (ax, ay) or (ax, -ay); affine coordinates canonical (< p). madd-2008-s.
+// The accumulator of this chain is kept "loose": X < 8p, Y < 4p (ZZ, ZZZ < 2p as products), so the
+// exits skip the conditional subtractions; every other formula and the packed storage (8p < 2^384)
+// accept loose inputs, because they use X and Y only as product operands (x29_add, x29_dbl:
+// 2Y < 8p) or map them through a product (k_tree_out).
 template <class F>
 DEV void x29_madd(X29<F>& p, const F& ax, const F& ay_in, bool neg) {
     using O = Ops29<F>;
@@ -151,29 +155,27 @@ DEV void x29_madd(X29<F>& p, const F& ax, const F& ay_in, bool neg) {
     F U2, S2, P, R;
     O::mul(U2, ax, p.zz);
     O::mul(S2, ay, p.zzz);
-    O::template sub<2>(P, U2, p.x);  // < 4p
-    O::template sub<2>(R, S2, p.y);  // < 4p
-    if (O::zero4(P)) {
-        if (O::zero4(R))
+    O::template sub<8>(P, U2, p.x);  // < 10p
+    O::template sub<4>(R, S2, p.y);  // < 6p
+    if (O::template zero_lt<16>(P)) {
+        if (O::template zero_lt<8>(R))
             x29_from_aff_dbl(p, ax, ay);
         else
             x29_set_inf(p);
         return;
     }
     F PP, PPP, Q, t, w;
-    O::sqr(PP, P);
+    O::template sqr_b<16>(PP, P);    // P.c1 < 10p
     O::mul(PPP, P, PP);
     O::mul(Q, p.x, PP);
-    O::sqr(t, R);
+    O::sqr(t, R);                    // R.c1 < 6p
     O::template sub<2>(w, t, PPP);   // < 4p
     O::add(t, Q, Q);                 // < 4p
-    O::template sub<4>(w, w, t);     // X3 < 8p
-    O::template reduce<8>(w);        // < 2p
-    O::template sub<2>(t, Q, w);     // < 4p
-    O::mul(t, R, t);
+    O::template sub<4>(w, w, t);     // X3 < 8p (loose)
+    O::template sub<8>(t, Q, w);     // < 10p
+    O::mul(t, t, R);                 // (t, R): the second operand's c1 must stay < 8p
     O::mul(S2, p.y, PPP);
-    O::template sub<2>(p.y, t, S2);  // < 4p
-    O::template reduce<4>(p.y);
+    O::template sub<2>(p.y, t, S2);  // Y3 < 4p (loose)
     p.x = w;
     O::mul(p.zz, p.zz, PP);
     O::mul(p.zzz, p.zzz, PPP);
@@ -195,8 +197,8 @@ DEV void x29_add(X29<F>& p, const X29<F>& q) {
     O::mul(S2, q.y, p.zzz);
     O::template sub<2>(P, U2, U1);
     O::template sub<2>(R, S2, S1);
-    if (O::zero4(P)) {
-        if (O::zero4(R))
+    if (O::template zero_lt<4>(P)) {
+        if (O::template zero_lt<4>(R))
             x29_dbl(p);
         else
             x29_set_inf(p);

@@ -41,6 +41,11 @@ struct Q29 {  // constants (see tools/gen_mont_asm.py's sibling computation in D
                                         0x0279c289, 0x1d91dd2e, 0x0869759a, 0x0b1ba7b6, 0x0bff34d2, 0x00447a8e, 0x00000034};
     static constexpr uint32_t P8[14] = {0x1ffd5558, 0x1fbfffff, 0x07ffff73, 0x1fffeb15, 0x1b120f55, 0x0a83dac3, 0x17ece61a,
                                         0x04f38512, 0x1b23ba5c, 0x10d2eb35, 0x16374f6c, 0x17fe69a4, 0x0088f51c, 0x00000068};
+    static constexpr uint32_t P16[14] = {0x1ffaaab0, 0x1f7fffff, 0x0ffffee7, 0x1fffd62a, 0x16241eab, 0x1507b587,
+                                         0x0fd9cc34, 0x09e70a25, 0x164774b8, 0x01a5d66b, 0x0c6e9ed9, 0x0ffcd349,
+                                         0x0111ea39, 0x000000d0};
+    // j p mod 2^29 = 2^29 - j 0x5555 (P[0] = 2^29 - 0x5555): INV5555 = 0x5555^-1 mod 2^32
+    static constexpr uint32_t INV5555 = 0xfffcfffdu;
     // R2 mod p (Montgomery one), R1 = 2^384 mod p (REDC by it maps x R2 -> x R1), R2^2 / R1 mod p (x R1 -> x R2)
     static constexpr uint32_t ONE[14] = {0x03a9fb84, 0x0ba00690, 0x071288f1, 0x0f59bcc5, 0x126cb614, 0x0585bf36, 0x1b85ac3d,
                                          0x1cf856fa, 0x1891ecbd, 0x1a7eec05, 0x155a88f0, 0x0741ac6d, 0x1317c30f, 0x00000009};
@@ -53,8 +58,8 @@ struct Q29 {  // constants (see tools/gen_mont_asm.py's sibling computation in D
 
 template <int K>
 DEV constexpr uint32_t kp29(int i) {
-    static_assert(K == 1 || K == 2 || K == 4 || K == 8, "multiple of p");
-    return K == 1 ? Q29::P[i] : K == 2 ? Q29::P2[i] : K == 4 ? Q29::P4[i] : Q29::P8[i];
+    static_assert(K == 1 || K == 2 || K == 4 || K == 8 || K == 16, "multiple of p");
+    return K == 1 ? Q29::P[i] : K == 2 ? Q29::P2[i] : K == 4 ? Q29::P4[i] : K == 8 ? Q29::P8[i] : Q29::P16[i];
 }
 
 DEV void f29_set(F29& r, const uint32_t (&c)[14]) {
@@ -208,6 +213,18 @@ DEV bool f29_zero4(const F29& x) {
     f29_csub<2>(y);
     return f29_zero2(y);
 }
+// x == 0 mod p for x < K p (K <= 16). x == j p for some j < K exactly when limb 0 (x mod 2^29, limbs
+// are normalized) is j p mod 2^29 = 2^29 - j 0x5555: a multiply and a compare reject every other
+// value, and only a candidate pays for the reduction and the full comparison.
+template <int K>
+DEV bool f29_zero_lt(const F29& x) {
+    const uint32_t v0 = x.v[0];
+    const bool cand = v0 == 0 || ((1u << 29) - v0) * Q29::INV5555 < (uint32_t)K;
+    if (!cand) return false;
+    F29 y = x;
+    f29_reduce<K>(y);
+    return f29_zero2(y);
+}
 // canonical (< p) from < 2p
 DEV void f29_canon(F29& x) { f29_csub<1>(x); }
 
@@ -249,10 +266,12 @@ DEV void f2_29_mul(F2_29& r, const F2_29& a, const F2_29& b) {
     r.c1 = c1;
 }
 // (a0 + a1 u)^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u
+// KB: bound of a.c1 in multiples of p (the subtraction adds KB p)
+template <int KB = 8>
 DEV void f2_29_sqr(F2_29& r, const F2_29& a) {
     F29 s, d, t, c0, c1;
     f29_add(s, a.c0, a.c1);
-    f29_sub<8>(d, a.c0, a.c1);
+    f29_sub<KB>(d, a.c0, a.c1);
     f29_add(t, a.c0, a.c0);
     f29_mul(c0, s, d);
     f29_mul(c1, t, a.c1);
@@ -278,6 +297,14 @@ struct Ops29<F29> {
     }
     static DEV bool zero2(const F29& x) { return f29_zero2(x); }
     static DEV bool zero4(const F29& x) { return f29_zero4(x); }
+    template <int K>
+    static DEV bool zero_lt(const F29& x) {
+        return f29_zero_lt<K>(x);
+    }
+    template <int KB>
+    static DEV void sqr_b(F29& r, const F29& a) {
+        f29_mul(r, a, a);
+    }
     static DEV bool is_zero_raw(const F29& x) { return f29_is_zero_raw(x); }
     static DEV void zero(F29& r) { f29_zero(r); }
     static DEV void one(F29& r) { f29_one(r); }
@@ -302,6 +329,14 @@ struct Ops29<F2_29> {
     }
     static DEV bool zero2(const F2_29& x) { return f29_zero2(x.c0) && f29_zero2(x.c1); }
     static DEV bool zero4(const F2_29& x) { return f29_zero4(x.c0) && f29_zero4(x.c1); }
+    template <int K>
+    static DEV bool zero_lt(const F2_29& x) {
+        return f29_zero_lt<K>(x.c0) && f29_zero_lt<K>(x.c1);
+    }
+    template <int KB>
+    static DEV void sqr_b(F2_29& r, const F2_29& a) {
+        f2_29_sqr<KB>(r, a);
+    }
     static DEV bool is_zero_raw(const F2_29& x) { return f29_is_zero_raw(x.c0) && f29_is_zero_raw(x.c1); }
     static DEV void zero(F2_29& r) {
         f29_zero(r.c0);

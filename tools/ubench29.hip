@@ -55,6 +55,7 @@ __global__ void k_curve(const Xyzz<S>* acc0, const Aff<S>* pts, int n, unsigned*
         T px, py; to29<S>(px, p.x); to29<S>(py, p.y);
         x29_madd(A, px, py, neg);
     }
+    { Xyzz<S> tmp; st29<S>(&tmp, A); ld29<S>(A, &tmp); }  // loose madd outputs survive the packed layout
     xyzz_add(a, q); x29_add(A, Q);
     xyzz_dbl(a, a); x29_dbl(A);
     Xyzz<S> b;

@@ -15,6 +15,8 @@
  */
 #include "oracle.h"
 
+#include <omp.h>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -480,14 +482,21 @@ static uint64_t digit(const uint64_t *s, int start, int c) {
 static int canon_is_one(const uint64_t *s) { return s[0] == 1 && !s[1] && !s[2] && !s[3]; }
 static int canon_is_zero(const uint64_t *s) { return !(s[0] | s[1] | s[2] | s[3]); }
 
+/* Windows are independent (ark-ec's VariableBaseMSM with its `parallel` feature splits the same way);
+ * orc_set_threads(k > 1) runs them on k OpenMP threads for the all-cores baseline. Same result. */
+static int g_threads = 1;
+void orc_set_threads(int k) { g_threads = k < 1 ? 1 : k; }
+int orc_get_threads(void) { return g_threads; }
+
 #define DEFINE_MSM(G)                                                                         \
     static void G##_msm(G##_jac *res_out, const G##_aff *bases, const uint64_t (*sc)[4], size_t n) { \
         int c = msm_c(n);                                                                     \
         int nb = 255;                                                                         \
         int nw = (nb + c - 1) / c;                                                            \
         G##_jac *ws = (G##_jac *)malloc(sizeof(G##_jac) * nw);                                \
-        G##_jac *bk = (G##_jac *)malloc(sizeof(G##_jac) * ((1u << c) - 1));                  \
+        _Pragma("omp parallel for schedule(dynamic, 1) num_threads(g_threads) if (g_threads > 1)") \
         for (int w = 0; w < nw; ++w) {                                                        \
+            G##_jac *bk = (G##_jac *)malloc(sizeof(G##_jac) * ((1u << c) - 1));              \
             int w_start = w * c;                                                              \
             G##_jac res;                                                                      \
             G##_set_inf(&res);                                                                \
@@ -508,6 +517,7 @@ static int canon_is_zero(const uint64_t *s) { return !(s[0] | s[1] | s[2] | s[3]
                 G##_add(&res, &res, &run);                                                    \
             }                                                                                 \
             ws[w] = res;                                                                      \
+            free(bk);                                                                         \
         }                                                                                     \
         G##_jac tot;                                                                          \
         G##_set_inf(&tot);                                                                    \
@@ -517,7 +527,6 @@ static int canon_is_zero(const uint64_t *s) { return !(s[0] | s[1] | s[2] | s[3]
         }                                                                                     \
         G##_add(res_out, &tot, &ws[0]);                                                       \
         free(ws);                                                                             \
-        free(bk);                                                                             \
     }
 DEFINE_MSM(g1)
 DEFINE_MSM(g2)
@@ -889,22 +898,36 @@ static void sc_round(mlsc_t *s, const fr_t *challenge, fr_t *evals) {
         fr_zero(&evals[t]);
     }
     size_t half = s->len / 2;
-    for (size_t b = 0; b < half; ++b) {
-        for (int t = 0; t <= deg; ++t) {
-            for (int p = 0; p < s->nprod; ++p) {
-                fr_t prod, u, v;
-                fr_one(&prod);
-                for (int j = 0; j < s->plen[p]; ++j) {
-                    const fr_t *tb = s->tab[s->pidx[p][j]];
-                    fr_mul(&u, &tb[2 * b], &omt[t]);
-                    fr_mul(&v, &tb[2 * b + 1], &tf[t]);
-                    fr_add(&u, &u, &v);
-                    fr_mul(&prod, &prod, &u);
+    /* pairs b split over g_threads (all-cores baseline); per-thread sums added in thread order:
+     * modular addition is exact, so the message is the same for any split */
+    int nth = (g_threads > 1 && half >= 64) ? g_threads : 1;
+    fr_t *part = (fr_t *)malloc(sizeof(fr_t) * (size_t)nth * (deg + 1));
+#pragma omp parallel num_threads(nth) if (nth > 1)
+    {
+        int id = omp_get_thread_num();
+        fr_t *ev = part + (size_t)id * (deg + 1);
+        for (int t = 0; t <= deg; ++t) fr_zero(&ev[t]);
+#pragma omp for schedule(static)
+        for (size_t b = 0; b < half; ++b) {
+            for (int t = 0; t <= deg; ++t) {
+                for (int p = 0; p < s->nprod; ++p) {
+                    fr_t prod, u, v;
+                    fr_one(&prod);
+                    for (int j = 0; j < s->plen[p]; ++j) {
+                        const fr_t *tb = s->tab[s->pidx[p][j]];
+                        fr_mul(&u, &tb[2 * b], &omt[t]);
+                        fr_mul(&v, &tb[2 * b + 1], &tf[t]);
+                        fr_add(&u, &u, &v);
+                        fr_mul(&prod, &prod, &u);
+                    }
+                    fr_add(&ev[t], &ev[t], &prod);
                 }
-                fr_add(&evals[t], &evals[t], &prod);
             }
         }
     }
+    for (int id = 0; id < nth; ++id)
+        for (int t = 0; t <= deg; ++t) fr_add(&evals[t], &evals[t], &part[(size_t)id * (deg + 1) + t]);
+    free(part);
 }
 
 /* ============================================================== mKZG */

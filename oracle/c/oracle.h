@@ -61,6 +61,9 @@ int orc_prove(const orc_csr *A, const orc_csr *B, const orc_csr *C, const uint8_
               const uint8_t *w, size_t nw_len, const orc_pp *pp, int mode, uint64_t inj_seed, uint8_t *out,
               size_t cap, size_t *out_len);
 const char *orc_last_error(void);
+/* OpenMP threads for the MSM windows and sumcheck rounds (default 1: the reference is single-threaded) */
+void orc_set_threads(int k);
+int orc_get_threads(void);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,8 @@ def lib():
         L.orc_msm_g2.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_commit.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
         L.orc_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_set_threads.argtypes = [ctypes.c_int]
+        L.orc_get_threads.restype = ctypes.c_int
         L.orc_prove.restype = ctypes.c_int
         L.orc_prove.argtypes = [
             ctypes.POINTER(Csr),
@@ -213,6 +215,11 @@ def open_(pp, table_bytes, nv, point_bytes):
     pf = ctypes.create_string_buffer(96 + 8 + 96 * nv)
     lib().orc_open(pp.h, table_bytes, nv, point_bytes, ev, pf)
     return ev.raw, pf.raw
+
+
+def set_threads(k):
+    """OpenMP threads for the oracle's MSM windows and sumcheck rounds (1 = the reference's single thread)."""
+    lib().orc_set_threads(int(k))
 
 
 def prove(mats, v_bytes, w_bytes, pp, mode=0, inj_seed=0):

@@ -35,8 +35,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # measured VALU ceilings of the curve additions the MSM kernels run (tools/ubench29.hip with all 256 CUs
-# busy, profiles/r01_ubench29.txt): mixed additions per second
-MADD_CEILING = {"msm_acc_g2": 1.96e9, "msm_acc_g1": 5.78e9}
+# busy, profiles/r01_ubench29_loose.txt, current loose-accumulator code): mixed additions per second
+MADD_CEILING = {"msm_acc_g2": 2.216e9, "msm_acc_g1": 6.041e9}
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
 KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
@@ -367,7 +367,7 @@ def main():
             roof["valu"] = {
                 "unit": "mixed additions/s",
                 "ceiling": MADD_CEILING[dom],
-                "ceiling_source": "tools/ubench29.hip, all CUs busy (profiles/r01_ubench29.txt)",
+                "ceiling_source": "tools/ubench29.hip, all CUs busy, L2-resident points (profiles/r01_ubench29_loose.txt)",
                 # per launch, live duration (shares the GPU with the other proofs in flight)
                 "achieved_per_launch": round(d["ops"] / d["launches"] / avg_s, 1),
                 "frac_per_launch": round(d["ops"] / d["launches"] / avg_s / MADD_CEILING[dom], 4),

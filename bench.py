@@ -16,10 +16,12 @@ hashing threads per rank) overlaps other proofs' GPU work instead of idling the 
 value = constraints proved per second over the timed region (whole job). The single-proof latency
 and the index-cached-transcript variant are reported beside it.
 
-N > 1: one process per GPU (torch.distributed.run); every proof is sharded over the ranks
-(hypercube blocks; per-round partials exchanged by an on-node shared-memory allgather, one
-communicator per proof in flight; --comm rccl uses RCCL AllGather instead), so "scaling" is
-"strong" (total work per step fixed).
+N > 1: one process per GPU (torch.distributed.run). Default (--shard batch): every rank proves its
+own P proofs per step, with no data-path exchange ("scaling": "weak"; value = all ranks' proofs / the
+max-over-ranks time). The same proofs split over all ranks are reported beside it as
+value_proof_sharded: hypercube blocks, with per-round partials exchanged by an on-node shared-memory
+allgather, one communicator per proof in flight; --comm rccl uses RCCL AllGather instead.
+--shard proof makes that the headline ("strong").
 
 Output: ONE JSON line on rank 0 (metric, value, roofline of the dominant kernel measured live with
 HIP events on the library's stream, cpu_baseline from the test oracle on a bounded sample).

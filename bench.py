@@ -1,27 +1,31 @@
 #!/usr/bin/env python
 """bench.py — R1CS constraints proved per second (BASELINE.json metric) on N MI355X.
 
-One proof = one complete `MLArgumentForR1CS::prove` (/root/reference/src/lib.rs:58-146) of a
-synthetic uniform-3n R1CS instance (2^20 constraints, |v| = 32, nnz = 3n) with the
+One proof = one complete `MLArgumentForR1CS::prove` (/root/reference/src/lib.rs:58-146) with the
 witness already resident in HBM: Fiat-Shamir transcript (including absorbing A, B, C on every
 proof), G1 commit MSM, two mKZG openings (G2 MSMs), SpMVs, eq tables, both sumchecks, proof
 serialization. Setup (keygen), index and witness upload are outside the timed region, as in
 benchmark.rs:26-35.
 
-One step = a batch of P = --proofs-per-step proofs (default 64); the K timed steps run as one
-continuous pipeline of K x P proofs through spx_prove_many with B = --inflight (default 16) host
-worker threads, each with its own HIP stream and MSM workspace, each proving its share back to
-back, so the sequential host Blake2s absorption of the matrices (~150 MB per proof, one pool of
-hashing threads per rank) overlaps other proofs' GPU work instead of idling the GPU.
-value = constraints proved per second over the timed region (whole job). The single-proof latency
-and the index-cached-transcript variant are reported beside it.
+Workload (BASELINE config C3): the "circuit-3n" synthetic R1CS at 2^20 constraints, |v| = 32,
+nnz = 3n: ONE index (A, B, C fixed) and W = --witnesses DISTINCT satisfying
+witnesses (default: one per proof of a step), so every proof has its own transcript, challenges,
+scalars and gather streams.
 
-N > 1: one process per GPU (torch.distributed.run). Default (--shard batch): every rank proves its
-own P proofs per step, with no data-path exchange ("scaling": "weak"; value = all ranks' proofs / the
-max-over-ranks time). The same proofs split over all ranks are reported beside it as
-value_proof_sharded: hypercube blocks, with per-round partials exchanged by an on-node shared-memory
-allgather, one communicator per proof in flight; --comm rccl uses RCCL AllGather instead.
---shard proof makes that the headline ("strong").
+One step = P = --proofs-per-step proofs (default 64) over the W witnesses; the K timed steps run
+as one continuous pipeline of K x P proofs through spx_prove_many with B = --inflight (default 16)
+host worker threads, each with its own HIP stream and MSM workspace, so the sequential host Blake2s
+absorption of the matrices (~150 MB per proof, one pool of hashing threads per rank) overlaps other
+proofs' GPU work. value = constraints proved per second over the timed region (whole job).
+Beside it: single-proof latency (with and without the index-cached transcript), the index-cached
+throughput, BASELINE config C2 (2^18, sumcheck-only, commitment stubbed) with its own HBM roofline,
+and CPU baselines (test oracle: 1 core at 2^14, all cores at --cpu-all-log-n).
+
+N > 1: one process per GPU (torch.distributed.run). Default (--shard proof): every proof is split
+over all ranks (hypercube blocks, per-round partials exchanged by an on-node
+shared-memory allgather, one communicator per proof in flight; --comm rccl uses RCCL). Total work
+per step is fixed ("scaling": "strong"). --shard batch makes every rank prove its own P proofs
+("weak"); the other mode's value is reported beside the headline.
 
 Output: ONE JSON line on rank 0 (metric, value, roofline of the dominant kernel measured live with
 HIP events on the library's stream, cpu_baseline from the test oracle on a bounded sample).
@@ -36,56 +40,30 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# measured VALU ceilings of the curve additions the MSM kernels run (tools/ubench29.hip with all 256 CUs
-# busy, profiles/r01_ubench29_loose.txt, current loose-accumulator code): mixed additions per second
-MADD_CEILING = {"msm_acc_g2": 2.216e9, "msm_acc_g1": 6.041e9}
+# VALU issue peak: 1024 SIMDs x 32 lanes per cycle x 2.4 GHz (MI355X_MICROARCH.md: a wave64 VALU
+# instruction issues over 2 cycles on a SIMD-32; = the 157.3 TFLOPS FP32 vector spec / 2 per FMA)
+VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 2.0
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_kernels.json")
+ISSUE_FILE = os.path.join(ROOT, "profiles", "r02_ubench_issue.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
-KSYM = {"sc1_round": "k_sc1_round", "sc2_round": "k_sc2_round", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
+KSYM = {"sc1_round": "k_sc1_round<true>", "sc2_round": "k_sc2_round<true>", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
         "open_level": "k_open_level", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
         "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq >", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
+          "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]
+HBM_KERNELS = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand"]
+KIND_NAMES = {0: "uniform-3n", 1: "ref-shaped", 3: "circuit-3n"}
 
 
-VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
-
-
-def valu_issue(ms_per_proof, dom):
-    """Compute-side roofline of the whole proof: the VALU wave-instructions every proof kernel issues
-    (rocprofv3 SQ_INSTS_VALU pass, tools/valu_summary.py -> profiles/pmc_valu.json) at the full issue
-    rate (4 cycles per wave-instruction on each of the 1024 SIMDs), against the measured time per proof."""
-    try:
-        d = json.load(open(VALU_FILE))
-    except (OSError, ValueError):
-        return None
-    ideal = d["ideal_valu_ms_per_proof"]
-    k = d["kernels"].get(KSYM.get(dom, ""), {})
-    return {"ideal_ms_per_proof": round(ideal, 3), "ms_per_proof": round(ms_per_proof, 3),
-            "frac": round(ideal / ms_per_proof, 4),
-            "dominant_kernel_ideal_ms_per_proof": round(k.get("ideal_valu_ms_per_proof", 0.0), 3),
-            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU, %g proofs, %g GHz)" % (d["proofs"], d["clock_ghz"])}
-
-
-def pmc_traffic(kname):
-    """HBM bytes per launch of `kname` from the committed rocprofv3 PMC passes (tools/pmc_summary.py)."""
+def pmc_kernel(kname):
+    """per-launch counters of `kname` from the committed rocprofv3 PMC passes (tools/pmc_summary.py)"""
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
         return None
     sym = KSYM.get(kname)
-    rec = d.get("kernels", {}).get(sym) if sym else None
-    if not rec or rec.get("traffic_bytes") is None:
-        return None
-    return rec["traffic_bytes"]
-
-
-KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
-          "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]
-
-
-def jobs_per_rank_step(P, world, sharded_head):
-    """proofs one rank's GPU completes per step: P in batch mode; P / world of each proof's work sharded"""
-    return P if not sharded_head else P / world * 1.0
+    return d.get("kernels", {}).get(sym) if sym else None
 
 
 def load_product():
@@ -96,26 +74,36 @@ def load_product():
     return mod
 
 
-def synth_instance(spx, kind, log_n, log_v, seed):
+def synth_instance(spx, kind, log_n, log_v, seed, n_wit, wseed0):
+    """the index's CSR views and n_wit witnesses (kind 3: distinct seeds wseed0..; else the generator's one)"""
     L = spx.lib()
-    L.spx_synth_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    L.spx_synth_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                   ctypes.POINTER(ctypes.c_void_p)]
     L.spx_synth_csr.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(spx._CCsr)]
     L.spx_synth_z.argtypes = [ctypes.c_void_p]
     L.spx_synth_z.restype = ctypes.c_void_p
     L.spx_synth_nnz.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.spx_synth_nnz.restype = ctypes.c_uint64
+    L.spx_synth_witnesses.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
     L.spx_synth_free.argtypes = [ctypes.c_void_p]
     h = ctypes.c_void_p()
-    spx._check(L.spx_synth_create(kind, log_n, log_v, seed, 0, ctypes.byref(h)))
+    spx._check(L.spx_synth_create(kind, log_n, log_v, seed, wseed0, ctypes.byref(h)))
     mats = []
     for m in range(3):
         c = spx._CCsr()
         spx._check(L.spx_synth_csr(h, m, ctypes.byref(c)))
         mats.append(c)
     n = 1 << log_n
-    z = ctypes.string_at(L.spx_synth_z(h), 32 * n)
+    if kind == 3:
+        buf = ctypes.create_string_buffer(32 * n * n_wit)
+        spx._check(L.spx_synth_witnesses(h, wseed0, n_wit, buf))
+        base = ctypes.addressof(buf)
+        zs = [ctypes.string_at(base + 32 * n * i, 32 * n) for i in range(n_wit)]
+        del buf
+    else:
+        zs = [ctypes.string_at(L.spx_synth_z(h), 32 * n)]
     nnz = sum(L.spx_synth_nnz(h, m) for m in range(3))
-    return h, mats, z, nnz
+    return h, mats, zs, nnz
 
 
 def index_from_c(spx, ctx, mats):
@@ -125,10 +113,7 @@ def index_from_c(spx, ctx, mats):
     return h
 
 
-def cpu_baseline(log_n, log_v, seconds_cap, threads=1):
-    """Test-oracle C prover (reference-faithful algorithms) on a bounded sample: one thread (the
-    reference is single-threaded as configured), or `threads` OpenMP threads over the MSM windows and
-    sumcheck pairs (what ark-ec's `parallel` feature would split)."""
+def oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
     so = os.path.join(ROOT, "oracle", "liboracle.so")
     if not os.path.exists(so):
@@ -137,30 +122,42 @@ def cpu_baseline(log_n, log_v, seconds_cap, threads=1):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     import oracle_c as oc
 
-    inst = oc.Instance(0, log_n, log_v, 0x5EED0000 + log_n)
-    pp = oc.PP.keygen(log_n, 0xC0FFEE)
+    return oc
+
+
+def cpu_baseline(kind, log_n, log_v, seconds_cap, threads=1, pp_bytes=None, stub=False, max_reps=3):
+    """Test-oracle C prover (reference-faithful algorithms: log_n eq tables, degree-(log_n+2) sumcheck,
+    hash-map eval_on_x, duplicated-scalar G2 MSMs, ark-ec Pippenger) on a bounded sample of the same
+    workload: one thread (the reference is single-threaded as configured), or `threads` OpenMP
+    threads over the MSM windows and sumcheck pairs (what ark-ec's `parallel` feature would split)."""
+    oc = oracle()
+    inst = oc.Instance(kind, log_n, log_v, 0x5EED0000 + log_n, 0xB0B0 if kind == 3 else 0)
+    pp = None if stub else (oc.PP.load(pp_bytes) if pp_bytes else oc.PP.keygen(log_n, 0xC0FFEE))
     oc.set_threads(threads)
     reps, t_total = 0, 0.0
     try:
         while True:
             t0 = time.perf_counter()
-            oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, pp, 0, 0)
+            oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, pp, 0, 0, commitment_stub=stub)
             t_total += time.perf_counter() - t0
             reps += 1
-            if t_total >= seconds_cap or reps >= 3:
+            if t_total >= seconds_cap or reps >= max_reps:
                 break
     finally:
         oc.set_threads(1)
     per = t_total / reps
     return {
-        "value": (1 << log_n) / per,
+        "value": round((1 << log_n) / per, 1),
         "unit": "constraints/s",
         "cores": threads,
         "kind": "port",
-        "sample": "oracle/c reference-faithful prover (log_n eq tables, degree-(log_n+2) sumcheck, "
-        "duplicated-scalar G2 MSMs, ark-ec Pippenger%s), uniform-3n 2^%d, |v|=%d, %d proof(s), %.2f s each, FS"
-        % ("" if threads == 1 else ", %d OpenMP threads over MSM windows and sumcheck pairs" % threads,
-           log_n, 1 << log_v, reps, per),
+        "sample": "oracle/c reference-faithful prover%s (log_n eq tables, degree-(log_n+2) sumcheck, hash-map "
+        "eval_on_x%s%s), %s 2^%d, |v|=%d, %d proof(s), %.2f s each, FS"
+        % (" with the commitment stubbed (C2)" if stub else "",
+           "" if stub else ", duplicated-scalar G2 MSMs, ark-ec Pippenger",
+           "" if threads == 1 else ", %d OpenMP threads over %ssumcheck pairs" % (threads, "" if stub else "MSM windows and "),
+           KIND_NAMES.get(kind, str(kind)), log_n, 1 << log_v, reps, per),
+        "log_n": log_n,
     }
 
 
@@ -172,30 +169,141 @@ def host_cores():
         return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
+def issue_costs():
+    """measured cycles per wave-instruction at 1 and 2 waves per SIMD (tools/ubench_issue.hip)"""
+    try:
+        txt = open(ISSUE_FILE).read()
+    except OSError:
+        return None
+    out = {}
+    for line in txt.splitlines():
+        if "cycles per wave-instruction" in line:
+            name = line.split("waves/SIMD")[0].strip()
+            w = int(line.split("waves/SIMD")[1].split(":")[0])
+            cyc = float(line.split("ms,")[1].split("cycles")[0])
+            out["%s@%d" % (name, w)] = cyc
+    return out
+
+
+def kernel_stats(spx, L, hctx, per_proof_div):
+    """HIP-event statistics of ctx's launches since enabling, per proof; 'largest' = the launches of each
+    kernel with the most algorithmic bytes (round 1 of a sumcheck)"""
+    L.spx_kernel_stats_largest.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    stats = {}
+    for k, name in enumerate(KNAMES):
+        cnt, kms, by, ops = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        spx._check(L.spx_kernel_stats(hctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
+        spx._check(L.spx_kernel_ops(hctx.h, k, ctypes.byref(ops)))
+        bc, bms, bby = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        spx._check(L.spx_kernel_stats_largest(hctx.h, k, ctypes.byref(bc), ctypes.byref(bms), ctypes.byref(bby)))
+        if cnt.value:
+            stats[name] = {"launches": cnt.value / per_proof_div, "ms": kms.value / per_proof_div,
+                           "bytes": by.value / per_proof_div, "ops": ops.value / per_proof_div,
+                           "largest": {"launches": bc.value, "ms": bms.value, "bytes": bby.value}}
+    return stats
+
+
+def roofline_valu(stats, dom):
+    """dominant MSM kernel: VALU issue (SQ_INSTS_VALU per launch from the committed PMC pass) over the
+    live HIP-event launch duration, against the chip's VALU issue peak; HBM side as secondary fields."""
+    d = stats[dom]
+    avg_s = d["ms"] / d["launches"] / 1e3
+    per_launch = d["bytes"] / d["launches"]
+    pm = pmc_kernel(dom) or {}
+    insts = pm.get("SQ_INSTS_VALU_per_launch")
+    roof = {
+        "kernel": KSYM.get(dom, dom),
+        "bound": "valu",
+        "unit": "G VALU wave-instructions/s",
+        "achieved": round(insts / avg_s / 1e9, 1) if insts else None,
+        "peak": round(VALU_PEAK_WAVE_INSTR / 1e9, 1),
+        "frac": round(insts / avg_s / VALU_PEAK_WAVE_INSTR, 4) if insts else None,
+        "traffic": pm.get("traffic_bytes"),
+        "avg_launch_us": round(avg_s * 1e6, 2),
+        "valu_insts_per_launch": insts,
+        "valu_source": "profiles/pmc_kernels.json (rocprofv3 --pmc SQ_INSTS_VALU, one proof in flight, same build)",
+        "note": "integer big-number VALU work (v_mad_u64_u32 limb products), no MFMA; live HIP-event duration with "
+        "one proof at a time",
+    }
+    ic = issue_costs()
+    if ic and insts:
+        # instruction-mix ceiling: v_mad_u64_u32 is ~3/4 of the kernel's VALU instructions
+        c1 = ic.get("v_mad_u64_u32@1")
+        roof["issue_costs_cycles"] = ic
+        if c1:
+            roof["frac_vs_mad_u64_rate_one_wave"] = round(insts * c1 / (1024 * 2.4e9) / avg_s, 4)
+    roof["hbm"] = {
+        "algorithmic_bytes_per_launch": per_launch,
+        "achieved_GBs": round(per_launch / avg_s / 1e9, 1),
+        "peak_GBs": HBM_PEAK_GBS,
+        "frac": round(per_launch / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+        "traffic_bytes_per_launch": pm.get("traffic_bytes"),
+        "traffic_over_algorithmic": round(pm["traffic_bytes"] / per_launch, 3) if pm.get("traffic_bytes") else None,
+        "traffic_source": "profiles/pmc_kernels.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
+    }
+    if d.get("ops"):
+        roof["mixed_additions_per_s_live"] = round(d["ops"] / d["launches"] / avg_s, 1)
+    return roof
+
+
+def roofline_hbm(stats):
+    """dominant HBM-streaming kernel (largest device time per proof among the sumcheck / SpMV / eq / fold
+    kernels), priced on its largest launches (round 1: the tables stream from HBM; later rounds shrink
+    into the caches and are launch-latency bound)"""
+    cands = [k for k in HBM_KERNELS if k in stats]
+    if not cands:
+        return None
+    dom = max(cands, key=lambda k: stats[k]["ms"])
+    d = stats[dom]
+    big = d["largest"]
+    avg_s = big["ms"] / big["launches"] / 1e3
+    per_launch = big["bytes"] / big["launches"]
+    ach = per_launch / avg_s / 1e9
+    pm = pmc_kernel(dom) or {}
+    return {"kernel": KSYM.get(dom, dom), "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("traffic_bytes_largest"),
+            "bytes_per_launch": per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
+            "all_launches": {"launches_per_proof": d["launches"], "ms_per_proof": round(d["ms"], 4),
+                             "GBs": round(d["bytes"] / (d["ms"] / 1e3) / 1e9, 1)},
+            "note": "algorithmic bytes of the kernel's largest launch / its HIP-event duration, one proof at a time"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--log-n", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=["c3", "c2"],
+                    help="c3: full prove + commit (BASELINE configs C3-C5); c2: sumcheck-only, commitment stubbed")
+    ap.add_argument("--log-n", type=int, default=None, help="default 20 (c3) / 18 (c2)")
     ap.add_argument("--log-v", type=int, default=5)
-    ap.add_argument("--kind", type=int, default=0, help="0 uniform-3n, 1 ref-shaped")
+    ap.add_argument("--kind", type=int, default=3, help="3 circuit-3n (distinct witnesses), 0 uniform-3n, 1 ref-shaped")
+    ap.add_argument("--witnesses", type=int, default=0, help="distinct witnesses (kind 3; default: one per proof of a step)")
     ap.add_argument("--mode", default="fs", choices=["fs", "injected"])
-    ap.add_argument("--cpu-log-n", type=int, default=14)
+    ap.add_argument("--cpu-log-n", type=int, default=14, help="1-core CPU baseline sample size")
+    ap.add_argument("--cpu-all-log-n", type=int, default=18, help="all-cores CPU baseline sample size")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
-    ap.add_argument("--shard", default="batch", choices=["batch", "proof"],
-                    help="N > 1 headline: 'batch' = every rank proves its own proofs (weak scaling, no data-path "
-                    "exchange); 'proof' = every proof split over all ranks (strong scaling, per-round exchange)")
-    ap.add_argument("--no-sharded", action="store_true",
-                    help="N > 1 with --shard batch: skip the secondary proof-sharded measurement")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 (sumcheck-only) line of the default run")
+    ap.add_argument("--shard", default="proof", choices=["batch", "proof"],
+                    help="N > 1 headline: 'proof' = every proof split over all ranks (strong, per-round exchange); "
+                    "'batch' = every rank proves its own proofs (weak, no data-path exchange)")
+    ap.add_argument("--no-other", action="store_true", help="N > 1: skip the other shard mode's measurement")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
-                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather")
+                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (needs --inflight 1)")
     ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts)")
     ap.add_argument("--proofs-per-step", type=int, default=64,
                     help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
     args = ap.parse_args()
+    stub = args.config == "c2"
+    log_n = args.log_n or (18 if stub else 20)
+    log_v = args.log_v
+    if args.comm == "rccl" and args.inflight != 1:
+        # one RCCL communicator per proof in flight, driven by independent threads: their device
+        # collectives can reach shared hardware queues in different orders on different ranks (deadlock)
+        raise SystemExit("--comm rccl needs --inflight 1 (see INTEGRATION.md)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -221,44 +329,49 @@ def main():
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
     # 16 hardware queues per process (HIP default 4): a proof's small latency-bound kernels (sumcheck
     # rounds, bucket-weighting levels) then queue behind fewer of the other proofs' MSM launches
-    # (measured 33.5 vs 31.1 M constraints/s at 2^20; 2 ranks on one GPU 23.9 vs 18.3)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     spx = load_product()
+    L = spx.lib()
     B = max(1, args.inflight)
     P = max(B, (args.proofs_per_step + B - 1) // B * B)  # proofs per step; each worker proves P / B of them
     # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
     device = 0 if os.environ.get("SPX_BENCH_SAME_GPU") == "1" else local
     sharded_head = world > 1 and args.shard == "proof"
-    # batch mode (and N = 1): contexts with the local communicator, every rank proves whole proofs
-    ctxs = [spx.Context(device) for _ in range(B)]
-    ctx = ctxs[0]
-    # proof-sharded contexts (N > 1): one communicator per proof in flight, every proof split over the ranks
-    sctxs = []
-    if world > 1 and (sharded_head or not args.no_sharded):
-        sctxs = [spx.Context(device) for _ in range(B)]
+    need_batch = world == 1 or not sharded_head or not args.no_other
+    need_sharded = world > 1 and (sharded_head or not args.no_other)
+
+    def make_sharded(k):
+        cs = [spx.Context(device) for _ in range(k)]
         if args.comm == "rccl":
-            uid = [[spx.comm_unique_id() for _ in range(B)] if rank == 0 else None]
+            uid = [[spx.comm_unique_id() for _ in range(k)] if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            for k, c in enumerate(sctxs):
-                c.set_comm_rccl(uid[0][k], rank, world)
+            for j, c in enumerate(cs):
+                c.set_comm_rccl(uid[0][j], rank, world)
         else:
             name = [spx.shm_name() if rank == 0 else None]
             dist.broadcast_object_list(name, src=0)
-            for k, c in enumerate(sctxs):
-                c.set_comm_shm("%s_%d" % (name[0], k), rank, world)
+            for j, c in enumerate(cs):
+                c.set_comm_shm("%s_%d" % (name[0], j), rank, world)
+        return cs
 
-    log_n, log_v = args.log_n, args.log_v
+    ctxs = [spx.Context(device) for _ in range(B)] if need_batch else []
+    sctxs = make_sharded(B) if need_sharded else []
+    ctx = (ctxs or sctxs)[0]
+
     n = 1 << log_n
+    W = (args.witnesses or P) if args.kind == 3 else 1
     t0 = time.perf_counter()
-    syn, mats, z, nnz = synth_instance(spx, args.kind, log_n, log_v, 0x5EED0000 + log_n)
+    syn, mats, zs, nnz = synth_instance(spx, args.kind, log_n, log_v, 0x5EED0000 + log_n, W, 0xB0B0)
     t_gen = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pp = spx.MLProofForR1CS.setup(ctx, log_n, 0xC0FFEE)
+    pp = None if stub else spx.MLProofForR1CS.setup(ctx, log_n, 0xC0FFEE)
     t_setup = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pk = spx.IndexPK(ctx, index_from_c(spx, ctx, mats), log_n)
+    pk = spx.IndexPK(ctxs[0], index_from_c(spx, ctxs[0], mats), log_n) if ctxs else None
     spk = spx.IndexPK(sctxs[0], index_from_c(spx, sctxs[0], mats), log_n) if sctxs else None
-    wit = spx.Witness(ctx, z[: 32 << log_v], z[32 << log_v :])
+    wits = [spx.Witness(ctx, z[: 32 << log_v], z[32 << log_v :]) for z in zs]
+    v0 = zs[0][: 32 << log_v]
+    del zs
     t_index = time.perf_counter() - t0
 
     def barrier():
@@ -273,67 +386,80 @@ def main():
         return r, time.perf_counter() - t0
 
     def batch_fn(cs, k, steps, cached=False):
-        return lambda: spx.MLArgumentForR1CS.prove_many(cs, k, [wit] * (P * steps), pp, mode=args.mode, seed=7,
-                                                        cached=cached)
+        wl = [wits[i % W] for i in range(P * steps)]
+        return lambda: spx.MLArgumentForR1CS.prove_many(cs, k, wl, pp, mode=args.mode, seed=7, cached=cached,
+                                                        commitment_stub=stub)
 
-    def single_fn(k):
+    def single_fn(c, k, cached=False):
         def run():
             for _ in range(args.steps):
-                r = spx.MLArgumentForR1CS.prove_witness(k, wit, pp, mode=args.mode, seed=7)
+                r = spx.MLArgumentForR1CS.prove_witness(k, wits[0], pp, mode=args.mode, seed=7, cached=cached,
+                                                        commitment_stub=stub)
             return r
         return run
+
+    def check_batch(proofs, ref=None):
+        ref = ref or proofs[:W]
+        assert all(p == ref[i % W] for i, p in enumerate(proofs)), "proofs of the same witness differ"
+        assert len(set(ref)) == len(ref), "distinct witnesses gave equal proofs"
+        return ref
 
     # headline configuration
     hctxs, hpk = (sctxs, spk) if sharded_head else (ctxs, pk)
     hctx = hctxs[0]
     batch_fn(hctxs, hpk, max(1, args.warmup))()
-    L = spx.lib()
     if not args.no_stats:
         spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
     # ---- timed region (headline): K steps x P full proofs, pipelined over B workers
     proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps))
     stats = {}
     if not args.no_stats:
-        for k, name in enumerate(KNAMES):
-            cnt, kms, by, ops = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-            spx._check(L.spx_kernel_stats(hctx.h, k, ctypes.byref(cnt), ctypes.byref(kms), ctypes.byref(by)))
-            spx._check(L.spx_kernel_ops(hctx.h, k, ctypes.byref(ops)))
-            if cnt.value:
-                # per proof: ctx 0 proves P / B proofs per step
-                per = args.steps * (P // B)
-                stats[name] = {"launches": cnt.value / per, "ms": kms.value / per, "bytes": by.value / per,
-                               "ops": ops.value / per}
+        stats = kernel_stats(spx, L, hctx, args.steps * (P // B))  # ctx 0 proves P / B proofs per step
         spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
-    assert all(p == proofs[0] for p in proofs), "concurrent proofs differ"
-    proof = proofs[0]
-    # ---- single-proof latency (one proof at a time) and its phase split
-    p1, elapsed_single = timed(single_fn(hpk))
-    assert p1 == proof, "single proof differs from the batched one"
+    ref = check_batch(proofs)
+    # ---- single-proof latency (one proof at a time), with and without the index-cached transcript
+    p1, elapsed_single = timed(single_fn(hctx, hpk))
+    assert p1 == ref[0], "single proof differs from the batched one"
     phases = hctx.last_timings()
-    # ---- index-cached transcript variant (matrix absorption moved to index time; bit-identical)
+    if not args.no_stats:  # kernel durations with one proof at a time (no other proof sharing the GPU)
+        spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
+    p1c, elapsed_single_c = timed(single_fn(hctx, hpk, cached=True))
+    assert p1c == ref[0], "cached-transcript single proof differs"
+    phases_c = hctx.last_timings()
+    alone = {}
+    if not args.no_stats:
+        alone = kernel_stats(spx, L, hctx, args.steps)
+        spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
+    # ---- index-cached transcript throughput (matrix absorption moved to index time; bit-identical)
     p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True))
-    assert all(p == proof for p in p2), "cached-transcript proof differs"
-    # ---- N > 1, batch headline: the same proofs split over all ranks (throughput and latency)
-    ms_s = ms_s1 = None
-    if sctxs and not sharded_head:
-        batch_fn(sctxs, spk, 1)()
-        p3, el = timed(batch_fn(sctxs, spk, args.steps))
-        assert all(p == proof for p in p3), "proof-sharded proof differs"
-        p4, el1 = timed(single_fn(spk))
-        assert p4 == proof, "proof-sharded single proof differs"
-        ms_s, ms_s1 = el / args.steps * 1e3, el1 / args.steps * 1e3
+    check_batch(p2, ref)
+    # ---- N > 1: the other shard mode (throughput, and the proof-sharded single-proof latency)
+    other = None
+    if world > 1 and not args.no_other:
+        octxs, opk = (ctxs, pk) if sharded_head else (sctxs, spk)
+        batch_fn(octxs, opk, 1)()
+        p3, el = timed(batch_fn(octxs, opk, args.steps))
+        check_batch(p3, ref)
+        el1 = None
+        if not sharded_head:
+            p4, el1 = timed(single_fn(octxs[0], opk))
+            assert p4 == ref[0], "proof-sharded single proof differs"
+        other = [el, el1]
 
     ms = elapsed / args.steps * 1e3  # per step (P proofs)
     ms_c = elapsed_cached / args.steps * 1e3
     ms_1 = elapsed_single / args.steps * 1e3
+    ms_1c = elapsed_single_c / args.steps * 1e3
+    ms_o = ms_o1 = None
     if dist is not None:
         import torch
 
-        t = torch.tensor([ms, ms_c, ms_1, ms_s or 0.0, ms_s1 or 0.0], dtype=torch.float64)
+        t = torch.tensor([ms, ms_c, ms_1, ms_1c, (other[0] / args.steps * 1e3) if other else 0.0,
+                          (other[1] / args.steps * 1e3) if other and other[1] else 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, ms_c, ms_1 = float(t[0]), float(t[1]), float(t[2])
-        if ms_s is not None:
-            ms_s, ms_s1 = float(t[3]), float(t[4])
+        ms, ms_c, ms_1, ms_1c = float(t[0]), float(t[1]), float(t[2]), float(t[3])
+        if other:
+            ms_o, ms_o1 = float(t[4]), (float(t[5]) or None)
     # whole-job throughput: in batch mode every rank proves P proofs per step, sharded all ranks share them
     jobs = P * (1 if sharded_head else world)
     if rank != 0:
@@ -342,51 +468,37 @@ def main():
         return
 
     roof = None
-    if stats:
-        # dominant kernel = largest share of a proof's GPU time when it runs alone (rocprofv3, one proof
-        # in flight: profiles/*kernel_stats_inflight1*.csv). Live durations under P proofs in flight
-        # overlap, so the latency-bound weighting-tree launches would otherwise look longest.
-        dom = "msm_acc_g2" if "msm_acc_g2" in stats else max(stats, key=lambda k: stats[k]["ms"])
-        d = stats[dom]
-        avg_s = d["ms"] / d["launches"] / 1e3
-        per_launch = d["bytes"] / d["launches"]
-        ach = per_launch / avg_s / 1e9
-        roof = {
-            "kernel": dom,
-            "bound": "hbm",
-            "achieved": round(ach, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(dom),
-            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
-            "bytes_per_launch": per_launch,
-            "avg_launch_us": round(avg_s * 1e6, 2),
-            "note": "algorithmic bytes / live HIP-event duration; MSM bucket accumulation is integer-VALU bound (see DESIGN.md)",
-        }
-        if dom in MADD_CEILING and d["ops"]:
-            per_proof_ops = d["ops"]  # mixed additions of one proof
-            roof["valu"] = {
-                "unit": "mixed additions/s",
-                "ceiling": MADD_CEILING[dom],
-                "ceiling_source": "tools/ubench29.hip, all CUs busy, L2-resident points (profiles/r01_ubench29_loose.txt)",
-                # per launch, live duration (shares the GPU with the other proofs in flight)
-                "achieved_per_launch": round(d["ops"] / d["launches"] / avg_s, 1),
-                "frac_per_launch": round(d["ops"] / d["launches"] / avg_s / MADD_CEILING[dom], 4),
-                # whole job: this kernel's additions of every proof in the timed region / wall time
-                "achieved_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3), 1),
-                "frac_job": round(per_proof_ops * (P if sharded_head else jobs) / (ms / 1e3) / MADD_CEILING[dom], 4),
-            }
-    if roof is not None:
-        vi = valu_issue(ms / jobs_per_rank_step(P, world, sharded_head), roof["kernel"])
-        if vi:
-            roof["valu_issue"] = vi
+    if alone:
+        if stub:
+            roof = roofline_hbm(alone)
+        else:
+            dom = "msm_acc_g2" if "msm_acc_g2" in alone else max(alone, key=lambda k: alone[k]["ms"])
+            roof = roofline_valu(alone, dom)
+            if dom in stats:  # the same kernel while 16 proofs share the GPU
+                d = stats[dom]
+                roof["avg_launch_us_shared"] = round(d["ms"] / d["launches"] * 1e3, 2)
+            hb = roofline_hbm(alone)
+            if hb:
+                roof["hbm_kernels"] = hb
     cpu = cpu_all = None
     if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds)
-        cpu_all = cpu_baseline(args.cpu_log_n, args.log_v, args.cpu_seconds, threads=host_cores())
+        cpu = cpu_baseline(args.kind, args.cpu_log_n if not stub else 16, log_v, args.cpu_seconds, stub=stub)
+        pp_bytes = None
+        if not stub and args.cpu_all_log_n != args.cpu_log_n:
+            # the GPU keygen's PP at the all-cores sample size, loaded into the oracle (CPU keygen at 2^18+
+            # would dominate the run)
+            pp_s = spx.MLProofForR1CS.setup(ctx, args.cpu_all_log_n, 0xC0FFEE)
+            pp_bytes = pp_s.serialize_uncompressed()
+            del pp_s
+        cpu_all = cpu_baseline(args.kind, args.cpu_all_log_n if not stub else log_n, log_v, args.cpu_seconds,
+                               threads=host_cores(), pp_bytes=pp_bytes, stub=stub, max_reps=1)
+        del pp_bytes
+    wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
+        KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
+        "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
+        args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, B)
     out = {
-        "metric": "R1CS constraints proved/sec at 2^%d" % log_n,
+        "metric": "R1CS constraints proved/sec at 2^%d%s" % (log_n, " (sumcheck-only, commitment stubbed)" if stub else ""),
         "value": round(jobs * n / (ms / 1e3), 1),
         "unit": "constraints/s",
         "n_gpus": world,
@@ -399,10 +511,10 @@ def main():
         "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
         "data": "synthetic",
         "config": {
-            "workload": "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, full prove + commit + 2 openings, %s transcript, "
-            "%d proofs per step, %d in flight" % ("uniform-3n" if args.kind == 0 else "ref-shaped", log_n, 1 << log_v,
-                                                   nnz, args.mode.upper(), P, B),
+            "workload": wl,
             "log_n": log_n,
+            "baseline_config": "C2" if stub else "C3",
+            "distinct_witnesses": W,
             "proofs_per_step": P,
             "proofs_in_flight": B,
             "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
@@ -410,26 +522,77 @@ def main():
         },
         "ms_per_proof_single": round(ms_1, 3),
         "value_single_proof": round(n / (ms_1 / 1e3), 1),
+        "ms_per_proof_single_cached_transcript": round(ms_1c, 3),
+        "value_single_proof_cached_transcript": round(n / (ms_1c / 1e3), 1),
         "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1),
         "ms_per_step_index_cached_transcript": round(ms_c, 3),
         "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
-        "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in stats.items()},
+        "phases_ms_cached_transcript": {k: round(v / 1e3, 3) for k, v in phases_c.items()},
+        "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in alone.items()},
+        "kernels_ms_per_proof_shared": {k: round(v["ms"], 3) for k, v in stats.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all,
         "setup_s": round(t_setup, 2),
         "index_s": round(t_index, 2),
         "gen_s": round(t_gen, 2),
-        "proof_bytes": len(proof),
+        "proof_bytes": len(ref[0]),
     }
-    if ms_s is not None:
-        # the same workload with every proof split over all ranks (hypercube blocks, per-round exchange)
-        out["value_proof_sharded"] = round(P * n / (ms_s / 1e3), 1)
-        out["ms_per_step_proof_sharded"] = round(ms_s, 3)
-        out["ms_per_proof_single_proof_sharded"] = round(ms_s1, 3)
+    if ms_o is not None:
+        if sharded_head:  # the other mode: every rank proves whole proofs
+            out["value_batch_weak"] = round(P * world * n / (ms_o / 1e3), 1)
+            out["ms_per_step_batch_weak"] = round(ms_o, 3)
+        else:
+            out["value_proof_sharded"] = round(P * n / (ms_o / 1e3), 1)
+            out["ms_per_step_proof_sharded"] = round(ms_o, 3)
+            out["ms_per_proof_single_proof_sharded"] = round(ms_o1, 3) if ms_o1 else None
+    if not stub and world == 1 and not args.no_c2:
+        out["c2"] = c2_line(spx, L, args, B)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def c2_line(spx, L, args, B):
+    """BASELINE config C2 beside the headline: 2^18 circuit-3n, sumcheck-only (commitment stubbed), the
+    same pipeline, its HBM-bound dominant kernel and the oracle's stubbed prover on all host cores."""
+    log_n, log_v, P = 18, args.log_v, 64
+    n = 1 << log_n
+    ctxs = [spx.Context(0) for _ in range(B)]
+    syn, mats, zs, nnz = synth_instance(spx, 3, log_n, log_v, 0x5EED0000 + log_n, P, 0xB0B0)
+    pk = spx.IndexPK(ctxs[0], index_from_c(spx, ctxs[0], mats), log_n)
+    wits = [spx.Witness(ctxs[0], z[: 32 << log_v], z[32 << log_v :]) for z in zs]
+    steps = max(1, args.steps)
+    run = lambda k: spx.MLArgumentForR1CS.prove_many(ctxs, pk, wits * k, None, mode=args.mode, seed=7,
+                                                     commitment_stub=True)
+    run(1)
+    t0 = time.perf_counter()
+    proofs = run(steps)
+    el = time.perf_counter() - t0
+    assert all(p == proofs[i % P] for i, p in enumerate(proofs))
+    spx._check(L.spx_kernel_stats_enable(ctxs[0].h, 1))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        p1 = spx.MLArgumentForR1CS.prove_witness(pk, wits[0], None, mode=args.mode, seed=7, cached=True,
+                                                 commitment_stub=True)
+    el1 = (time.perf_counter() - t0) / steps
+    stats = kernel_stats(spx, L, ctxs[0], steps)
+    spx._check(L.spx_kernel_stats_enable(ctxs[0].h, 0))
+    assert p1 == proofs[0]
+    res = {
+        "metric": "R1CS constraints proved/sec at 2^18 (sumcheck-only, commitment stubbed)",
+        "value": round(steps * P * n / el, 1),
+        "unit": "constraints/s",
+        "workload": "circuit-3n 2^18, |v|=%d, nnz=%d, %d distinct witnesses, FS transcript, %d in flight" % (
+            1 << log_v, nnz, P, B),
+        "ms_per_proof_single_cached_transcript": round(el1 * 1e3, 3),
+        "kernels_ms_per_proof": {k: round(v["ms"], 4) for k, v in stats.items()},
+        "roofline": roofline_hbm(stats),
+    }
+    if not args.no_cpu:
+        res["cpu_baseline_all_cores"] = cpu_baseline(3, log_n, log_v, args.cpu_seconds, threads=host_cores(), stub=True,
+                                                     max_reps=1)
+    return res
 
 
 if __name__ == "__main__":

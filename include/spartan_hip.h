@@ -61,6 +61,11 @@ typedef struct {
     int mode;            /* SPX_FS: Blake2s512Rng Fiat-Shamir (reference); SPX_INJECTED: SplitMix64(inj_seed) */
     uint64_t inj_seed;
     int cached_matrix_transcript; /* 1: resume the Blake2s state absorbed at spx_index time (bit-identical) */
+    int commitment_stub; /* 1: BASELINE config C2, "sumcheck-only, commitment stubbed": the proof prove()
+                            gives under a public parameter whose every group element is the identity
+                            (commitment, h and opening proofs = infinity; the z evaluations are still
+                            computed). No MSM runs and pp may be NULL. Not a sound proof: benchmark /
+                            parity mode of the sumcheck half of lib.rs:58-146. */
 } spx_prove_opts;
 
 const char *spx_last_error(void);
@@ -154,13 +159,16 @@ int spx_cs_is_satisfied(spx_cs *cs, int *ok);
 int spx_cs_matrices(spx_cs *cs, spx_csr *a, spx_csr *b, spx_csr *c, const uint8_t **v, const uint8_t **w);
 
 /* ---- synthetic instances (SURVEY §8(d) generators; SplitMix64, same draws as the test oracle) ----
- * kind 0 = uniform-3n (satisfiable, nnz = 3n), 1 = ref-shaped (TestSynthesizer, param = density).
+ * kind 0 = uniform-3n (satisfiable, nnz = 3n), 1 = ref-shaped (TestSynthesizer, param = density),
+ * 3 = circuit-3n (fixed index, nnz = 3n, many witnesses: param = witness seed of spx_synth_z).
  * spx_synth_csr fills views into the handle (valid until spx_synth_free). */
 typedef struct spx_synth spx_synth;
 int spx_synth_create(int kind, int log_n, int log_v, uint64_t seed, uint64_t param, spx_synth **out);
 uint64_t spx_synth_nnz(const spx_synth *s, int m);
 int spx_synth_csr(const spx_synth *s, int m, spx_csr *out);
 const uint8_t *spx_synth_z(const spx_synth *s);
+/* kind 3 only: the witnesses (z = v || w, canonical, 32 n bytes each) of seeds wseed0 .. wseed0 + count - 1 */
+int spx_synth_witnesses(const spx_synth *s, uint64_t wseed0, int count, uint8_t *z_out);
 int spx_synth_free(spx_synth *s);
 
 /* ---- live kernel statistics (HIP events on the library's stream, enabled per ctx) ----
@@ -183,6 +191,9 @@ enum {
 };
 int spx_kernel_stats_enable(spx_ctx *ctx, int on);
 int spx_kernel_stats(spx_ctx *ctx, int id, uint64_t *launches, double *ms, double *bytes);
+/* the same, restricted to the launches of `id` with the largest algorithmic bytes (e.g. round 1 of a
+ * sumcheck, where the tables stream from HBM) */
+int spx_kernel_stats_largest(spx_ctx *ctx, int id, uint64_t *launches, double *ms, double *bytes);
 /* unit operations counted for a kernel id: curve additions (upper bound: zero digits included) for
  * SPX_K_ACC_* (mixed) and SPX_K_ACCX_* (XYZZ); 0 for the others */
 int spx_kernel_ops(spx_ctx *ctx, int id, double *ops);

@@ -115,6 +115,60 @@ static void gen_uniform_3n(orc_inst *I, uint64_t seed) {
     }
 }
 
+/* ---- circuit-3n (kind 3): a fixed index with many satisfying witnesses (bench: distinct witnesses).
+ * Rows x < n - |v| define output o_x = perm[x] (Fisher-Yates of the private columns):
+ * (alpha, a) x (beta, b) = (1, o_x), a and b uniform over the variables defined so far; the last |v|
+ * rows are (alpha, a) x (1, One) = (alpha, a). Witness seed -> public inputs; the rest follows. */
+static void circuit_witness(orc_inst *I, uint64_t wseed) {
+    uint64_t n = I->n, nv = 1ULL << I->log_v;
+    sm64 w = {wseed};
+    fr_one(&I->z[0]);
+    for (uint64_t i = 1; i < nv; ++i) sm64_fr_nonzero(&w, &I->z[i]);
+    for (uint64_t x = 0; x + nv < n; ++x) {
+        fr_t t, u;
+        fr_mul(&t, &I->m[0].val[x], &I->z[I->m[0].col[x]]);
+        fr_mul(&u, &I->m[1].val[x], &I->z[I->m[1].col[x]]);
+        fr_mul(&I->z[I->m[2].col[x]], &t, &u);
+    }
+}
+static void gen_circuit_3n(orc_inst *I, uint64_t seed, uint64_t wseed) {
+    uint64_t n = I->n, nv = 1ULL << I->log_v;
+    sm64 r = {seed};
+    uint32_t *perm = (uint32_t *)malloc(4 * (n - nv + 1)), *avail = (uint32_t *)malloc(4 * n);
+    for (uint64_t i = 0; i < n - nv; ++i) perm[i] = (uint32_t)(nv + i);
+    for (uint64_t i = n - nv - 1; i >= 1; --i) {
+        uint64_t j = sm64_next(&r) % (i + 1);
+        uint32_t t = perm[i];
+        perm[i] = perm[j];
+        perm[j] = t;
+    }
+    uint64_t na = 0;
+    for (uint64_t i = 0; i < nv; ++i) avail[na++] = (uint32_t)i;
+    for (int k = 0; k < 3; ++k) mat_init(&I->m[k], n, n);
+    fr_t one;
+    fr_one(&one);
+    for (uint64_t x = 0; x < n; ++x) {
+        fr_t al, be;
+        uint32_t a = avail[sm64_next(&r) % na];
+        sm64_fr(&r, &al);
+        mat_push(&I->m[0], a, &al);
+        if (x + nv < n) {
+            uint32_t b = avail[sm64_next(&r) % na];
+            sm64_fr(&r, &be);
+            mat_push(&I->m[1], b, &be);
+            mat_push(&I->m[2], perm[x], &one);
+            avail[na++] = perm[x];
+        } else {
+            mat_push(&I->m[1], 0, &one);
+            mat_push(&I->m[2], a, &al);
+        }
+        for (int k = 0; k < 3; ++k) I->m[k].row_ptr[x + 1] = I->m[k].nnz;
+    }
+    free(perm);
+    free(avail);
+    circuit_witness(I, wseed);
+}
+
 /* ---- ref-shaped: TestSynthesizer (constraints.rs:39-110) + make_matrices_square ---- */
 typedef struct { uint64_t var; fr_t val; } assign_t; /* var = column index */
 static int cmp_u64(const void *a, const void *b) {
@@ -285,6 +339,8 @@ orc_inst *orc_gen(int kind, int log_n, int log_v, uint64_t seed, uint64_t param)
         gen_uniform_3n(I, seed);
     else if (kind == ORC_GEN_REF_SHAPED)
         gen_ref_shaped(I, seed, (int)param);
+    else if (kind == ORC_GEN_CIRCUIT_3N)
+        gen_circuit_3n(I, seed, param);
     else
         gen_ragged(I, seed, (int)(param & 0xFFFF), (int)(param >> 16));
     return I;
@@ -934,8 +990,23 @@ static void sc_round(mlsc_t *s, const fr_t *challenge, fr_t *evals) {
 static void to_canon_arr(uint64_t (*out)[4], const fr_t *a, size_t n) {
     for (size_t i = 0; i < n; ++i) fr_to_canon(out[i], &a[i]);
 }
+/* BASELINE config C2 ("sumcheck-only, commitment stubbed"): the proof prove() would output under
+ * the public parameter whose every group element is the identity. Commitment, h and every opening
+ * proof are the point at infinity and no MSM runs; the evaluations of z still do (they are on the
+ * transcript). orc_prove's mode bit 2 selects it; the product's spx_prove_opts.commitment_stub. */
+static _Thread_local int g_stub = 0;
 static void commit(buf_t *b, const orc_pp *pp, const fr_t *z, int nv) {
     size_t n = (size_t)1 << nv;
+    if (g_stub) {
+        g1_aff inf;
+        memset(&inf, 0, sizeof inf);
+        inf.inf = 1;
+        uint8_t c[48];
+        g1_compress(c, &inf);
+        buf_u64(b, (uint64_t)nv);
+        buf_put(b, c, 48);
+        return;
+    }
     uint64_t(*sc)[4] = malloc(32 * n);
     to_canon_arr(sc, z, n);
     g1_jac r;
@@ -952,6 +1023,17 @@ static void commit(buf_t *b, const orc_pp *pp, const fr_t *z, int nv) {
 static void open_(buf_t *b, fr_t *eval_out, const orc_pp *pp, const fr_t *z, int nv, const fr_t *pt) {
     size_t n = (size_t)1 << nv;
     mle_eval(eval_out, z, nv, pt);
+    if (g_stub) {
+        g2_aff inf;
+        memset(&inf, 0, sizeof inf);
+        inf.inf = 1;
+        uint8_t hb[96];
+        g2_compress(hb, &inf);
+        buf_put(b, hb, 96);
+        buf_u64(b, (uint64_t)nv);
+        for (int i = 0; i < nv; ++i) buf_put(b, hb, 96);
+        return;
+    }
     fr_t *r = (fr_t *)malloc(sizeof(fr_t) * n);
     memcpy(r, z, sizeof(fr_t) * n);
     fr_t *q = (fr_t *)malloc(sizeof(fr_t) * (n / 2 + 1));
@@ -1087,8 +1169,10 @@ int orc_prove(const orc_csr *A, const orc_csr *B, const orc_csr *C, const uint8_
     int log_n = ark_log2(n);
     if (!nv_len || (nv_len & (nv_len - 1))) return set_err("public input should be power of two"), 1;
     if (nv_len + nw_len != n) return set_err("|v| + |w| != number of variables"), 1;
-    if (pp->nv < log_n) return set_err("public parameter too small"), 1;
+    if (!(mode & 2) && (!pp || pp->nv < log_n)) return set_err("public parameter too small"), 1;
     int log_v = ark_log2(nv_len);
+    g_stub = (mode & 2) != 0;
+    mode &= 1;
     fs_t fs;
     fs_init(&fs, mode == 1, inj_seed);
     for (int m = 0; m < 3; ++m) feed_matrix(&fs, Ms[m]);
@@ -1105,7 +1189,7 @@ int orc_prove(const orc_csr *A, const orc_csr *B, const orc_csr *C, const uint8_
         if (fr_from_bytes(&z[nv_len + i], w + 32 * i)) return set_err("non-canonical field element"), 1;
     /* the PP used is the level-aligned suffix when pp->nv > log_n is not supported by the
        reference either (open indexes powers_of_h[i] with 2^(nv-i) points): require equality */
-    if (pp->nv != log_n) return set_err("public parameter nv != log_n"), 1;
+    if (!g_stub && pp->nv != log_n) return set_err("public parameter nv != log_n"), 1;
     buf_t pf = {0};
     size_t mark;
     /* round 1: commit */

@@ -29,7 +29,7 @@ typedef struct orc_inst orc_inst;
 typedef struct orc_pp orc_pp;
 
 /* ---- synthetic instances (oracle/py/gen.py, draw for draw) ---- */
-enum { ORC_GEN_UNIFORM_3N = 0, ORC_GEN_REF_SHAPED = 1, ORC_GEN_RAGGED = 2 };
+enum { ORC_GEN_UNIFORM_3N = 0, ORC_GEN_REF_SHAPED = 1, ORC_GEN_RAGGED = 2, ORC_GEN_CIRCUIT_3N = 3 /* param = witness seed */ };
 orc_inst *orc_gen(int kind, int log_n, int log_v, uint64_t seed, uint64_t param);
 uint64_t orc_inst_nnz(const orc_inst *I, int m);
 int orc_inst_log_v(const orc_inst *I);
@@ -55,7 +55,9 @@ void orc_open(const orc_pp *pp, const uint8_t *table, int nv, const uint8_t *poi
               uint8_t *proof_out);
 
 /* ---- full argument (lib.rs:58-146) ----
- * mode 0 = Fiat-Shamir (Blake2s512Rng transcript), 1 = injected challenges (SplitMix64(inj_seed)).
+ * mode 0 = Fiat-Shamir (Blake2s512Rng transcript), 1 = injected challenges (SplitMix64(inj_seed));
+ * OR 2 = commitment stubbed (BASELINE config C2: identity commitment and opening proofs, no MSM,
+ * pp may be NULL).
  * Returns 0 on success, else an error code (1 = InvalidArgument ...); *out_len = proof length. */
 int orc_prove(const orc_csr *A, const orc_csr *B, const orc_csr *C, const uint8_t *v, size_t nv_len,
               const uint8_t *w, size_t nw_len, const orc_pp *pp, int mode, uint64_t inj_seed, uint8_t *out,

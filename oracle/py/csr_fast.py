@@ -42,12 +42,16 @@ def eq_table(point):
 
 
 def sparse_eval(n, row_ptr, col, val_bytes, eqx, eqy):
-    """M(r_x, r_y) = sum_{(x, y, a) in M} a eq(r_x, x) eq(r_y, y); rows are x (constraints), columns y."""
+    """M(r_x, r_y) = sum_{(x, y, a) in M} a eq(r_x, x) eq(r_y, y); rows are x (constraints), columns y.
+    A row that repeats a column contributes only its last entry for it (eval_on_x's map insert,
+    r1cs_reader.rs:98-108)."""
     rp = list(row_ptr)
     acc = 0
     for x in range(n):
         ex = eqx[x]
+        row = {}
         for k in range(rp[x], rp[x + 1]):
-            a = int.from_bytes(val_bytes[32 * k : 32 * k + 32], "little")
-            acc += a * eqy[col[k]] % R * ex
+            row[col[k]] = int.from_bytes(val_bytes[32 * k : 32 * k + 32], "little")
+        for y, a in row.items():
+            acc += a * eqy[y] % R * ex
     return acc % R

@@ -16,6 +16,10 @@ Generators:
     (test_utils.rs:51-79) with ark-relations matrix conventions [upstream]: column 0 = One,
     instance variables next, witnesses after; each row's entries sorted by column with
     duplicate variables merged. Draws come from SplitMix64 instead of test_rng().
+  * `circuit_3n(log_n, log_v, seed, wseed)` — the benchmark's fixed index with many witnesses:
+    rows x < n - |v| define a fresh private variable o_x (Fisher-Yates permutation of the private
+    columns) by (alpha, a) x (beta, b) = (1, o_x) over variables defined earlier; the last |v| rows
+    are (alpha, a) x (1, One) = (alpha, a). `wseed` draws the public inputs; the rest follows.
   * `random_matrix(log_size, nnz, seed)` — restates test_utils.rs:18-37 (row lists in
     insertion order, unique (x, y) positions).
 A matrix is a list of n rows, each a list of (coeff, col) — ark-relations `Matrix<F>`.
@@ -80,6 +84,40 @@ def uniform_3n(log_n, log_v=5, seed=None):
         B.append([(beta, b)])
         C.append([(gamma, c)])
     nv = 1 << log_v
+    return A, B, C, z[:nv], z[nv:]
+
+
+def circuit_3n(log_n, log_v=5, seed=None, wseed=0):
+    n, nv = 1 << log_n, 1 << log_v
+    if seed is None:
+        seed = default_seed(log_n)
+    rng = SplitMix64(seed)
+    perm = list(range(nv, n))
+    for i in range(len(perm) - 1, 0, -1):
+        j = rng.next_u64() % (i + 1)
+        perm[i], perm[j] = perm[j], perm[i]
+    avail = list(range(nv))
+    A, B, C = [], [], []
+    for x in range(n):
+        a = avail[rng.next_u64() % len(avail)]
+        alpha = rng.next_fr()
+        A.append([(alpha, a)])
+        if x + nv < n:
+            b = avail[rng.next_u64() % len(avail)]
+            B.append([(rng.next_fr(), b)])
+            C.append([(1, perm[x])])
+            avail.append(perm[x])
+        else:
+            B.append([(1, 0)])
+            C.append([(alpha, a)])
+    w = SplitMix64(wseed)
+    z = [0] * n
+    z[0] = 1
+    for i in range(1, nv):
+        z[i] = w.next_fr_nonzero()
+    for x in range(n - nv):
+        (al, a), (be, b), (_one, o) = A[x][0], B[x][0], C[x][0]
+        z[o] = al * z[a] % R * be % R * z[b] % R
     return A, B, C, z[:nv], z[nv:]
 
 

@@ -73,7 +73,7 @@ def lib():
     return _lib
 
 
-GEN_UNIFORM_3N, GEN_REF_SHAPED, GEN_RAGGED = 0, 1, 2
+GEN_UNIFORM_3N, GEN_REF_SHAPED, GEN_RAGGED, GEN_CIRCUIT_3N = 0, 1, 2, 3
 
 
 class CsrMatrix:
@@ -222,8 +222,11 @@ def set_threads(k):
     lib().orc_set_threads(int(k))
 
 
-def prove(mats, v_bytes, w_bytes, pp, mode=0, inj_seed=0):
+def prove(mats, v_bytes, w_bytes, pp, mode=0, inj_seed=0, commitment_stub=False):
+    """mode 0 = FS, 1 = injected; commitment_stub: BASELINE config C2 (pp may be None)."""
     L = lib()
+    if commitment_stub:
+        mode |= 2
     A, B, C = (m.csr() for m in mats)
     n = mats[0].n
     cap = 64 * 1024 + 64 * n.bit_length() * 64
@@ -237,7 +240,7 @@ def prove(mats, v_bytes, w_bytes, pp, mode=0, inj_seed=0):
         len(v_bytes) // 32,
         w_bytes,
         len(w_bytes) // 32,
-        pp.h,
+        pp.h if pp is not None else None,
         mode,
         inj_seed,
         out,

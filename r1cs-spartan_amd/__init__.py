@@ -64,7 +64,8 @@ class _CCsr(ctypes.Structure):
 
 
 class _Opts(ctypes.Structure):
-    _fields_ = [("mode", ctypes.c_int), ("inj_seed", ctypes.c_uint64), ("cached_matrix_transcript", ctypes.c_int)]
+    _fields_ = [("mode", ctypes.c_int), ("inj_seed", ctypes.c_uint64), ("cached_matrix_transcript", ctypes.c_int),
+                ("commitment_stub", ctypes.c_int)]
 
 
 EXPORTED = [
@@ -381,8 +382,16 @@ class Witness:
             pass
 
 
-def _opts(mode, seed, cached):
-    return _Opts(1 if mode == "injected" else 0, int(seed), 1 if cached else 0)
+def _opts(mode, seed, cached, stub=False):
+    return _Opts(1 if mode == "injected" else 0, int(seed), 1 if cached else 0, 1 if stub else 0)
+
+
+def _pp_handle(pp, stub):
+    if pp is None:
+        if not stub:
+            raise InvalidArgument("a public parameter is required unless commitment_stub=True")
+        return None
+    return pp.h
 
 
 class MLProofForR1CS:
@@ -404,28 +413,32 @@ class MLArgumentForR1CS:
         return IndexPK(ctx, h, A.n.bit_length() - 1)
 
     @staticmethod
-    def prove(pk, v, w, pp, mode="fs", seed=0, cached=False):
-        """Proof bytes (ark-serialize compressed, proof.rs:10-20 field order)."""
+    def prove(pk, v, w, pp, mode="fs", seed=0, cached=False, commitment_stub=False):
+        """Proof bytes (ark-serialize compressed, proof.rs:10-20 field order).
+        commitment_stub=True is BASELINE config C2 (sumcheck-only): the proof prove() gives under a
+        public parameter whose every group element is the identity; no MSM runs and pp may be None."""
         vb, wb = _as_bytes(v), _as_bytes(w)
         cap = lib().spx_proof_size(pk.log_n, 0)
         out = ctypes.create_string_buffer(cap)
         n = ctypes.c_size_t(0)
-        o = _opts(mode, seed, cached)
-        _check(lib().spx_prove(pk.ctx.h, pk.h, vb, len(vb) // 32, wb, len(wb) // 32, pp.h, ctypes.byref(o), out, cap, ctypes.byref(n)))
+        o = _opts(mode, seed, cached, commitment_stub)
+        _check(lib().spx_prove(pk.ctx.h, pk.h, vb, len(vb) // 32, wb, len(wb) // 32, _pp_handle(pp, commitment_stub),
+                               ctypes.byref(o), out, cap, ctypes.byref(n)))
         return out.raw[: n.value]
 
     @staticmethod
-    def prove_witness(pk, wit, pp, mode="fs", seed=0, cached=False):
+    def prove_witness(pk, wit, pp, mode="fs", seed=0, cached=False, commitment_stub=False):
         cap = lib().spx_proof_size(pk.log_n, 0)
         out = ctypes.create_string_buffer(cap)
         n = ctypes.c_size_t(0)
-        o = _opts(mode, seed, cached)
-        _check(lib().spx_prove_witness(pk.ctx.h, pk.h, wit.h, pp.h, ctypes.byref(o), out, cap, ctypes.byref(n)))
+        o = _opts(mode, seed, cached, commitment_stub)
+        _check(lib().spx_prove_witness(pk.ctx.h, pk.h, wit.h, _pp_handle(pp, commitment_stub), ctypes.byref(o), out, cap,
+                                       ctypes.byref(n)))
         return out.raw[: n.value]
 
 
     @staticmethod
-    def prove_many(ctxs, pk, wits, pp, mode="fs", seed=0, cached=False):
+    def prove_many(ctxs, pk, wits, pp, mode="fs", seed=0, cached=False, commitment_stub=False):
         """Proves every witness in `wits` concurrently, one worker per context (spx_prove_many)."""
         cap = lib().spx_proof_size(pk.log_n, 0)
         n = len(wits)
@@ -433,8 +446,9 @@ class MLArgumentForR1CS:
         lens = (ctypes.c_size_t * max(n, 1))()
         ch = (ctypes.c_void_p * len(ctxs))(*[c.h for c in ctxs])
         wh = (ctypes.c_void_p * max(n, 1))(*[w.h for w in wits])
-        o = _opts(mode, seed, cached)
-        _check(lib().spx_prove_many(ch, len(ctxs), pk.h, wh, n, pp.h, ctypes.byref(o), out, cap, lens))
+        o = _opts(mode, seed, cached, commitment_stub)
+        _check(lib().spx_prove_many(ch, len(ctxs), pk.h, wh, n, _pp_handle(pp, commitment_stub), ctypes.byref(o), out,
+                                    cap, lens))
         raw = out.raw
         return [raw[i * cap : i * cap + lens[i]] for i in range(n)]
 

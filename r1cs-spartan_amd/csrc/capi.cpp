@@ -76,8 +76,14 @@ spx::ProveOpts opts_of(const spx_prove_opts* o) {
         p.mode = o->mode;
         p.seed = o->inj_seed;
         p.cached = o->cached_matrix_transcript != 0;
+        p.stub = o->commitment_stub != 0;
     }
     return p;
+}
+spx::PP* pp_of(spx_pp* pp, const spx::ProveOpts& o) {
+    if (pp) return pp->p.get();
+    if (!o.stub) spx::invalid("null public parameter");
+    return nullptr;
 }
 int copy_out(const std::vector<uint8_t>& v, uint8_t* out, size_t cap, size_t* len) {
     if (len) *len = v.size();
@@ -216,20 +222,25 @@ int spx_prove(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uint
               const spx_prove_opts* opts, uint8_t* out, size_t cap, size_t* len) {
     return guard([&] {
         set_dev(ctx);
+        if (!idx) spx::invalid("null prover key");
+        const spx::ProveOpts o = opts_of(opts);
+        spx::PP* P = pp_of(pp, o);
         auto W = spx::witness_upload(*ctx->c, v, nv, w, nw);
-        copy_out(spx::prove(*ctx->c, *idx->i, *W, *pp->p, opts_of(opts)), out, cap, len);
+        copy_out(spx::prove(*ctx->c, *idx->i, *W, P, o), out, cap, len);
     });
 }
 int spx_prove_witness(spx_ctx* ctx, spx_pk* idx, spx_witness* wit, spx_pp* pp, const spx_prove_opts* opts,
                       uint8_t* out, size_t cap, size_t* len) {
     return guard([&] {
         set_dev(ctx);
-        copy_out(spx::prove(*ctx->c, *idx->i, *wit->w, *pp->p, opts_of(opts)), out, cap, len);
+        if (!idx || !wit) spx::invalid("null prover key / witness");
+        const spx::ProveOpts o = opts_of(opts);
+        copy_out(spx::prove(*ctx->c, *idx->i, *wit->w, pp_of(pp, o), o), out, cap, len);
     });
 }
 int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, int nproofs, spx_pp* pp,
                    const spx_prove_opts* opts, uint8_t* out, size_t stride, size_t* lens) {
-    if (!ctxs || nctx < 1 || !idx || !wits || nproofs < 0 || !pp || !out || !lens) {
+    if (!ctxs || nctx < 1 || !idx || !wits || nproofs < 0 || !out || !lens) {
         g_err = "spx_prove_many: bad arguments";
         return SPX_INVALID_ARGUMENT;
     }
@@ -244,8 +255,10 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             return SPX_INVALID_ARGUMENT;
         }
     spx::ProveOpts base;
+    spx::PP* P = nullptr;
     try {
         base = opts_of(opts);
+        P = pp_of(pp, base);
     } catch (const spx::SpxError& e) {
         g_err = e.what();
         return e.code;
@@ -310,7 +323,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
                             throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
                         return &slots[i].h;
                     };
-                auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, *pp->p, o);
+                auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, P, o);
                 if (p.size() > stride) spx::invalid("proof buffer too small");
                 memcpy(out + (size_t)i * stride, p.data(), p.size());
                 lens[i] = p.size();
@@ -390,6 +403,17 @@ int spx_kernel_stats(spx_ctx* ctx, int id, uint64_t* launches, double* ms, doubl
     });
 }
 
+int spx_kernel_stats_largest(spx_ctx* ctx, int id, uint64_t* launches, double* ms, double* bytes) {
+    return guard([&] {
+        if (id < 0 || id >= SPX_K_COUNT) spx::invalid("bad kernel id");
+        set_dev(ctx);
+        ctx->c->sync();
+        auto& k = ctx->c->kprof;
+        if (launches) *launches = k.big_launches[id];
+        if (ms) *ms = k.big_ms[id];
+        if (bytes) *bytes = k.big_bytes[id];
+    });
+}
 int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
     return guard([&] {
         if (id < 0 || id >= SPX_K_COUNT) spx::invalid("bad kernel id");

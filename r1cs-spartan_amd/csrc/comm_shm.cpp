@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/spartan_hip.h"
 #include "prover.hpp"
@@ -48,11 +49,32 @@ struct ShmComm : Comm {
         name = "/" + nm;
         if (nm.find('/') != std::string::npos) invalid("shm comm: name must not contain '/'");
         len = kHdr + 2 * (size_t)world * kSlot;
-        int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
-        if (fd < 0) throw SpxError(kDevice, "shm_open failed for " + name);
-        if (ftruncate(fd, (off_t)len) != 0) {
-            close(fd);
-            throw SpxError(kDevice, "ftruncate failed for " + name);
+        // rank 0 creates the segment (O_EXCL: a leftover segment of that name is an error, never
+        // silently reused with stale counters) and sizes it, which zero-fills it; the others open
+        // the existing object only, waiting until it exists at its full size
+        int fd = -1;
+        if (r == 0) {
+            fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd < 0) throw SpxError(kDevice, "shm_open(O_EXCL) failed for " + name + " (name in use?)");
+            if (ftruncate(fd, (off_t)len) != 0) {
+                close(fd);
+                shm_unlink(name.c_str());
+                throw SpxError(kDevice, "ftruncate failed for " + name);
+            }
+        } else {
+            auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+                fd = shm_open(name.c_str(), O_RDWR, 0600);
+                if (fd >= 0) {
+                    struct stat st;
+                    if (fstat(fd, &st) == 0 && (size_t)st.st_size == len) break;
+                    close(fd);
+                    fd = -1;
+                }
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
+                    throw SpxError(kDevice, "shm comm: segment " + name + " not created by rank 0 in 600 s");
+                usleep(1000);
+            }
         }
         void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         close(fd);

@@ -46,6 +46,10 @@ struct KProf {
     std::vector<hipEvent_t> pool;
     uint64_t launches[16] = {0};
     double ms[16] = {0}, bytes[16] = {0}, ops[16] = {0};
+    // the launches moving the most algorithmic bytes per id (e.g. round 1 of a sumcheck: the
+    // HBM-streaming case; later rounds are small and cache-resident)
+    uint64_t big_launches[16] = {0};
+    double big_ms[16] = {0}, big_bytes[16] = {0};
     int cur_id = -1;
     hipEvent_t cur_a = nullptr;
     hipEvent_t get() {
@@ -79,6 +83,15 @@ struct KProf {
                 ms[r.id] += t;
                 bytes[r.id] += r.bytes;
                 ops[r.id] += r.ops;
+                const double top = big_launches[r.id] ? big_bytes[r.id] / big_launches[r.id] : 0.0;
+                if (r.bytes > top * 1.0001) {
+                    big_launches[r.id] = 0, big_ms[r.id] = 0, big_bytes[r.id] = 0;
+                }
+                if (r.bytes >= top * 0.9999) {
+                    big_launches[r.id] += 1;
+                    big_ms[r.id] += t;
+                    big_bytes[r.id] += r.bytes;
+                }
             }
             pool.push_back(r.a);
             pool.push_back(r.b);
@@ -86,7 +99,8 @@ struct KProf {
         open.clear();
     }
     void reset() {
-        for (int i = 0; i < 16; ++i) launches[i] = 0, ms[i] = 0, bytes[i] = 0, ops[i] = 0;
+        for (int i = 0; i < 16; ++i)
+            launches[i] = 0, ms[i] = 0, bytes[i] = 0, ops[i] = 0, big_launches[i] = 0, big_ms[i] = 0, big_bytes[i] = 0;
     }
 };
 extern thread_local KProf* g_kprof;  // set by the host for the calling thread

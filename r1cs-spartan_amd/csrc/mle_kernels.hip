@@ -11,6 +11,8 @@
 // the reduction order is fixed, and field addition is exact, so results are deterministic.
 #include "kernels.hpp"
 
+#include <stdexcept>
+
 namespace spx {
 
 thread_local KProf* g_kprof = nullptr;
@@ -331,6 +333,7 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
 
 // ------------------------------------------------------------------ mKZG open level (open.rs:42-45)
 // q[b] = r[2b+1] - r[2b];  r'[b] = r[2b] + p * q[b]   ( = r[2b](1-p) + r[2b+1] p )
+// q may be null (fold only: the commitment-stubbed mode evaluates z without quotients)
 __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
                                                          Fr* __restrict__ q, const Fr* __restrict__ point,
                                                          uint64_t half) {
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ 
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
         fe_sub(d, a1, a0);
-        st_fr(q + b, d);
+        if (q) st_fr(q + b, d);
         if (!rout) continue;  // quotient only (the shared level 0 of the openings)
         fe_mul(t, d, p);
         fe_add(t, a0, t);
@@ -388,8 +391,9 @@ void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* 
 
 void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
                      Fr* scratch_hi, hipStream_t s) {
-    // split k = klo + khi, each <= 12 (k <= 24)
+    // split k = klo + khi, each <= 13 (k <= 26): the scratch halves hold 2^13 entries
     int klo = (k + 1) / 2, khi = k - klo;
+    if (k < 0 || klo > 13) throw std::invalid_argument("launch_eq_table: more than 26 variables");
     hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev, klo, scratch_lo);
     hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev + klo, khi, scratch_hi);
     kp_begin(KP_EQ, s);
@@ -428,7 +432,7 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s) {
     kp_begin(KP_OPEN, s);
     hipLaunchKernelGGL(k_open_level, dim3(grid_for(half, 8192)), dim3(kThreads), 0, s, rin, rout, q, point, half);
-    kp_end(32.0 * (rout ? 4.0 : 3.0) * (double)half, s);  // read 2, write q (and r')
+    kp_end(32.0 * (2.0 + (q ? 1.0 : 0.0) + (rout ? 1.0 : 0.0)) * (double)half, s);  // read 2, write q and/or r'
 }
 
 }  // namespace spx

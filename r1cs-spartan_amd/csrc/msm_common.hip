@@ -204,8 +204,9 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* sca
     o.tot_refs = tot_refs;
     o.d_insts = (MsmInst*)ws->insts.ensure(sizeof(MsmInst) * ninst);
     auto* d_prefix = (uint64_t*)ws->prefix.ensure(8 * (ninst + 1));
-    HIPCHK(hipMemcpyAsync(o.d_insts, o.insts.data(), sizeof(MsmInst) * ninst, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_prefix, prefix.data(), 8 * (ninst + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(o.d_insts, ws->pin.stage(o.insts.data(), ninst), sizeof(MsmInst) * ninst,
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_prefix, ws->pin.stage(prefix.data(), ninst + 1), 8 * (ninst + 1), hipMemcpyHostToDevice, s));
     o.counts = (uint32_t*)ws->counts.ensure(4 * (nb + 1));
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
     uint32_t* cursor = (uint32_t*)ws->cursor.ensure(4 * (nb + 1));
@@ -263,6 +264,7 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* sca
     HIPCHK(hipcub::DeviceReduce::Max(t, tb, o.counts, d_max, nb, s));
     HIPCHK(hipMemcpyAsync(ws->h_max, d_max, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    ws->pin.reset();  // every copy staged so far (this batch's and the previous batch's tree tables) is done
     o.maxc = *ws->h_max;
     return o;
 }

@@ -3,6 +3,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -77,10 +78,35 @@ struct DBuf {
     }
 };
 
+// Pinned host staging for the small per-batch tables an MSM uploads (instance descriptors, scalar
+// prefixes, weighting-tree prefixes). A hipMemcpyAsync from pageable memory may read its source
+// after the call returns, so the source must outlive the copy: regions are bump-allocated and the
+// arena is reset only right after a stream synchronisation that covers every copy issued from it
+// (msm_sort's). Fixed capacity: nothing is ever reallocated under an in-flight copy.
+struct PinArena {
+    static constexpr size_t kCap = 256 << 10;
+    uint8_t* p = nullptr;
+    size_t used = 0;
+    PinArena() { HIPCHK(hipHostMalloc((void**)&p, kCap)); }
+    ~PinArena() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T* stage(const T* src, size_t count) {  // copy `count` items into the arena; returns the pinned copy
+        const size_t o = (used + 255) & ~(size_t)255, b = sizeof(T) * count;
+        if (o + b > kCap) throw std::runtime_error("MSM pinned staging arena exhausted");
+        used = o + b;
+        memcpy(p + o, src, b);
+        return (T*)(p + o);
+    }
+    void reset() { used = 0; }  // only after a sync covering every copy from the arena
+};
+
 struct MsmWorkspace {
     DBuf insts, prefix, redp, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, maxv,
         tprefix, keys_a, keys_b, vals_a;
     uint32_t* h_max = nullptr;
+    PinArena pin;
     MsmWorkspace() { HIPCHK(hipHostMalloc((void**)&h_max, sizeof(uint32_t))); }
     ~MsmWorkspace() {
         if (h_max) (void)hipHostFree(h_max);

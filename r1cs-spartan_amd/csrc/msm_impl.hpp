@@ -277,9 +277,11 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     uint64_t* d_wp = (uint64_t*)tp;
     uint32_t* d_cin = (uint32_t*)(tp + 8 * wp.size());
     uint32_t* d_noff = d_cin + cin.size();
-    HIPCHK(hipMemcpyAsync(d_wp, wp.data(), 8 * wp.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_cin, cin.data(), 4 * cin.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_noff, node_off.data(), 4 * node_off.size(), hipMemcpyHostToDevice, s));
+    // pinned staging: this function returns before the copies run (no sync), the vectors do not outlive it
+    HIPCHK(hipMemcpyAsync(d_wp, ws->pin.stage(wp.data(), wp.size()), 8 * wp.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_cin, ws->pin.stage(cin.data(), cin.size()), 4 * cin.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_noff, ws->pin.stage(node_off.data(), node_off.size()), 4 * node_off.size(),
+                          hipMemcpyHostToDevice, s));
     auto* TA = (Xyzz<F>*)ws->tree_a.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
     auto* TB = (Xyzz<F>*)ws->tree_b.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
     Xyzz<F>* A3[3] = {TA, TA + tot_nodes, TA + 2 * (size_t)tot_nodes};

@@ -34,6 +34,7 @@ Ctx::Ctx(int dev) : device(dev) {
     if (blocking) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     SPX_HIP(hipSetDevice(dev));
     SPX_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    SPX_HIP(hipHostMalloc((void**)&pin, kPinBytes));
     msm = msm_ws_create();
     comm.reset(new LocalComm());
 }
@@ -44,14 +45,9 @@ Ctx::~Ctx() {
     if (pin) (void)hipHostFree(pin);
     if (stream) (void)hipStreamDestroy(stream);
 }
-uint8_t* Ctx::pinned(size_t b) {
-    if (b > pin_bytes) {
-        if (pin) SPX_HIP(hipHostFree(pin));
-        size_t nb = std::max<size_t>(b, 1 << 20);
-        SPX_HIP(hipHostMalloc((void**)&pin, nb));
-        pin_bytes = nb;
-    }
-    return pin;
+uint8_t* Ctx::pin_at(size_t off, size_t bytes, size_t region) {
+    if (bytes > region || off + region > kPinBytes) throw SpxError(kDevice, "pinned staging region too small");
+    return pin + off;
 }
 
 static inline int ilog2(uint64_t x) { return 63 - __builtin_clzll(x); }
@@ -137,7 +133,7 @@ std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len) {
         return v;
     };
     uint64_t nv = u64();
-    if (nv < 1 || nv > 30) throw SpxError(kSerialization, "bad public parameter nv");
+    if (nv < 1 || nv > (uint64_t)kMaxLogN) throw SpxError(kSerialization, "bad public parameter nv (1..26 supported)");
     if (u64() != nv) throw SpxError(kSerialization, "powers_of_g length != nv");
     pp_alloc_raw(*P, (int)nv);
     std::vector<size_t> g1_pos(nv), g2_pos(nv);
@@ -231,7 +227,7 @@ static void upload_affine(const std::vector<Affine<F>>& v, A* dst, hipStream_t s
 }
 
 std::unique_ptr<PP> pp_generate(Ctx& C, int nv, uint64_t seed) {
-    if (nv < 1 || nv > 28) invalid("keygen: nv out of range");
+    if (nv < 1 || nv > kMaxLogN) invalid("keygen: nv out of range (1..26 supported)");
     auto P = std::make_unique<PP>();
     SplitMix64 rng{seed};
     HFr gs = rng.fr(), hs = rng.fr();
@@ -381,6 +377,42 @@ static void upload_sparse(Ctx& C, DevSparse& D, const std::vector<uint64_t>* ptr
     }
 }
 
+// CSC copy of M for eval_on_x (rows ascending within a column). The reference inserts every
+// (xy_combine(x, y), value) pair into a SparseMLExtensionMap (r1cs_reader.rs:98-108), so when a
+// row repeats a column only the LAST entry of that row survives; sum_over_y (r1cs_reader.rs:75-85)
+// keeps adding every entry, so only this copy drops the superseded ones.
+static void build_csc(const HostCsr& M, uint64_t n, std::vector<uint64_t>& cp, std::vector<uint32_t>& rows,
+                      std::vector<uint8_t>& vals) {
+    const uint64_t nnz = M.rp[n];
+    std::vector<uint8_t> dead(nnz, 0);
+    std::vector<uint64_t> last_row(n, ~0ull), last_k(n, 0);
+    uint64_t live = 0;
+    for (uint64_t x = 0; x < n; ++x)
+        for (uint64_t k = M.rp[x]; k < M.rp[x + 1]; ++k) {
+            const uint32_t y = M.col[k];
+            if (last_row[y] == x)
+                dead[last_k[y]] = 1;
+            else
+                ++live;
+            last_row[y] = x;
+            last_k[y] = k;
+        }
+    cp.assign(n + 1, 0);
+    for (uint64_t k = 0; k < nnz; ++k)
+        if (!dead[k]) cp[M.col[k] + 1]++;
+    for (uint64_t y = 0; y < n; ++y) cp[y + 1] += cp[y];
+    std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
+    rows.assign(live, 0);
+    vals.assign(32 * live, 0);
+    for (uint64_t x = 0; x < n; ++x)
+        for (uint64_t k = M.rp[x]; k < M.rp[x + 1]; ++k) {
+            if (dead[k]) continue;
+            const uint64_t pos = cur[M.col[k]]++;
+            rows[pos] = (uint32_t)x;
+            memcpy(&vals[32 * pos], &M.val[32 * k], 32);
+        }
+}
+
 static void feed_matrix(Blake2s& h, const HostCsr& m) {
     // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize }
     std::vector<uint8_t> buf;
@@ -418,6 +450,7 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
     const uint64_t n = mats[0].n;
     if (!is_pow2(n)) invalid("Matrix width should be a power of 2.");  // indexer.rs:49-51
     if (n < 2) invalid("at least 2 constraints are required");
+    if (n > (1ull << kMaxLogN)) invalid("more than 2^26 constraints are not supported");
     for (int m = 0; m < 3; ++m) check_csr(mats[m], n);
     I->n = n;
     I->log_n = ilog2(n);
@@ -442,24 +475,8 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
         for (int m = 0; m < 3; ++m) c3[m] = *ci[m], v3[m] = *vi[m];
         upload_sparse(C, I->rows, rps, c3, v3, lo, nl, err.as<int>());
     }
-    // columns (CSC, stable counting sort: rows ascending within a column) for eval_on_x
-    for (int m = 0; m < 3; ++m) {
-        const HostCsr& M = mats[m];
-        const uint64_t nnz = M.rp[n];
-        std::vector<uint64_t> cp(n + 1, 0);
-        for (uint64_t k = 0; k < nnz; ++k) cp[M.col[k] + 1]++;
-        for (uint64_t y = 0; y < n; ++y) cp[y + 1] += cp[y];
-        std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
-        cols[m].assign(nnz, 0);
-        vals[m].assign(32 * nnz, 0);
-        for (uint64_t x = 0; x < n; ++x)
-            for (uint64_t k = M.rp[x]; k < M.rp[x + 1]; ++k) {
-                uint64_t pos = cur[M.col[k]]++;
-                cols[m][pos] = (uint32_t)x;
-                memcpy(&vals[m][32 * pos], &M.val[32 * k], 32);
-            }
-        rps[m] = std::move(cp);
-    }
+    // columns (CSC, last entry of a repeated (x, y) kept) for eval_on_x
+    for (int m = 0; m < 3; ++m) build_csc(mats[m], n, rps[m], cols[m], vals[m]);
     upload_sparse(C, I->cols, rps, cols, vals, lo, nl, err.as<int>());
     {
         double e_rows = 0, e_cols = 0;
@@ -583,11 +600,12 @@ static void commit_launch(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, in
     inst.W = (uint32_t)P.g1_W;
     void* out = C.buf(Ctx::kSlotCommit, 4 * sizeof(Fq));
     msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out, C.stream);
-    SPX_HIP(hipMemcpyAsync(C.pinned(4 * sizeof(Fq)), out, 4 * sizeof(Fq), hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, 4 * sizeof(Fq), 4 << 10), out, 4 * sizeof(Fq),
+                           hipMemcpyDeviceToHost, C.stream));
 }
 static Affine<HFq> commit_finish(Ctx& C, int G) {
     C.sync();
-    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(C.pinned(4 * sizeof(Fq)));
+    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(C.pin_at(Ctx::kPinCommit, 4 * sizeof(Fq), 4 << 10));
     if (G == 1) return part;
     return sum_affine(allgather_affine(*C.comm, part));
 }
@@ -602,7 +620,6 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
 // (r_v, 0..0) (prover.rs:152) and in the one at r_y (prover.rs:275). It is computed once per proof,
 // launched right behind the commitment (before any challenge exists, overlapping the host's
 // absorption of the matrices) and handed to both open_z calls: a quarter of the proof's G2 work.
-static constexpr size_t kPinLvl0 = 1 << 17;  // pinned offset of the level-0 result (hp uses [0, 64 KiB))
 static bool lvl0_local(int L, int G) { return L - ilog2((uint64_t)G) >= 1; }
 static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank) {
     const uint64_t half = ((1ull << L) / G) / 2;
@@ -618,11 +635,11 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank
     const size_t xb = 4 * sizeof(Fq2);
     void* out = C.buf(Ctx::kSlotLvl0Out, xb);
     msm_run_g2(C.msm, &I, 1, P.g2_pre.as<G2Aff>(), q, out, C.stream);
-    SPX_HIP(hipMemcpyAsync(C.pinned(kPinLvl0 + xb) + kPinLvl0, out, xb, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, xb, 4 << 10), out, xb, hipMemcpyDeviceToHost, C.stream));
 }
 static Affine<HFq2> lvl0_finish(Ctx& C, int G) {
     C.sync();
-    Affine<HFq2> part = xyzz_bytes_to_affine<HFq2>(C.pinned(kPinLvl0 + 4 * sizeof(Fq2)) + kPinLvl0);
+    Affine<HFq2> part = xyzz_bytes_to_affine<HFq2>(C.pin_at(Ctx::kPinLvl0, 4 * sizeof(Fq2), 4 << 10));
     if (G == 1) return part;
     return sum_affine(allgather_affine(*C.comm, part));
 }
@@ -647,7 +664,9 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
     Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * std::max<uint64_t>(nl, 1));
     Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
                    C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
-    SPX_HIP(hipMemcpyAsync(pt, point.data(), 32 * L, hipMemcpyHostToDevice, C.stream));  // pageable: staged
+    uint8_t* ps = C.pin_at(Ctx::kPinStage, 32 * L, 64 << 10);
+    memcpy(ps, point.data(), 32 * L);
+    SPX_HIP(hipMemcpyAsync(pt, ps, 32 * L, hipMemcpyHostToDevice, C.stream));
     std::vector<MsmInst> insts(nloc - first);
     const Fr* rin = z_local;
     uint64_t qoff = 0;
@@ -674,7 +693,7 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
     void* out = C.buf(Ctx::kSlotOpenOut, 4 * sizeof(Fq2) * std::max(nm, 1));
     msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream);
     const size_t xb = 4 * sizeof(Fq2);
-    uint8_t* h = C.pinned(xb * nm + 32);
+    uint8_t* h = C.pin_at(Ctx::kPinOpen, xb * nm + 32, 56 << 10);
     if (nm) SPX_HIP(hipMemcpyAsync(h, out, xb * nm, hipMemcpyDeviceToHost, C.stream));
     SPX_HIP(hipMemcpyAsync(h + xb * nm, rin, 32, hipMemcpyDeviceToHost, C.stream));
     C.sync();
@@ -721,19 +740,60 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector
     res.eval = rg[0];
     Fr* qd = C.buf<Fr>(Ctx::kSlotTailQ, 32 * qs.size());
     void* out2 = C.buf(Ctx::kSlotTailOut, xb * tinsts.size());
-    SPX_HIP(hipMemcpyAsync(qd, qs.data(), 32 * qs.size(), hipMemcpyHostToDevice, C.stream));  // pageable: staged
+    uint8_t* hq = C.pin_at(Ctx::kPinTailIn, 32 * qs.size(), 32 << 10);
+    memcpy(hq, qs.data(), 32 * qs.size());
+    SPX_HIP(hipMemcpyAsync(qd, hq, 32 * qs.size(), hipMemcpyHostToDevice, C.stream));
     msm_run_g2(C.msm, tinsts.data(), (int)tinsts.size(), P.g2_pre.as<G2Aff>(), qd, out2, C.stream);
-    uint8_t* h2 = C.pinned(xb * tinsts.size());
+    uint8_t* h2 = C.pin_at(Ctx::kPinTailOut, xb * tinsts.size(), 32 << 10);
     SPX_HIP(hipMemcpyAsync(h2, out2, xb * tinsts.size(), hipMemcpyDeviceToHost, C.stream));
     C.sync();
     for (size_t k = 0; k < tinsts.size(); ++k) res.proofs[nloc + k] = xyzz_bytes_to_affine<HFq2>(h2 + xb * k);
     return res;
 }
 
-static void ser_open(Ser& s, const HFr& eval, const PP& P, const std::vector<Affine<HFq2>>& proofs) {
+// BASELINE config C2 (commitment stubbed): the opening under the all-identity public parameter.
+// The evaluation z(point) is computed exactly as open_z computes it (the same folds, no quotients,
+// no MSM); h and every level's proof are the identity.
+static OpenOut open_stub(Ctx& C, const Fr* z_local, int L, const std::vector<HFr>& point, int G) {
+    const int g = ilog2((uint64_t)G);
+    const uint64_t nl = (1ull << L) / G;
+    const int nloc = L - g;
+    OpenOut res;
+    res.proofs.assign(L, Affine<HFq2>{HFq2::zero(), HFq2::zero(), true});
+    Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
+    Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
+                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
+    uint8_t* h = C.pin_at(Ctx::kPinOpen, 32 * (L + 1), 56 << 10);
+    memcpy(h, point.data(), 32 * L);
+    SPX_HIP(hipMemcpyAsync(pt, h, 32 * L, hipMemcpyHostToDevice, C.stream));
+    const Fr* rin = z_local;
+    for (int i = 0; i < nloc; ++i) {
+        Fr* rout = bufs[i & 1];
+        launch_open_level(rin, rout, nullptr, pt + i, nl >> (i + 1), C.stream);
+        rin = rout;
+    }
+    SPX_HIP(hipMemcpyAsync(h + 32 * L, rin, 32, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    HFr rlast = ld_hfr(h + 32 * L);
+    if (G == 1) {
+        res.eval = rlast;
+        return res;
+    }
+    std::vector<HFr> rg = allgather_fr(*C.comm, {rlast});
+    for (int i = nloc; i < L; ++i) {
+        std::vector<HFr> nr(rg.size() / 2);
+        for (size_t b = 0; b < nr.size(); ++b) nr[b] = rg[2 * b] + point[i] * (rg[2 * b + 1] - rg[2 * b]);
+        rg.swap(nr);
+    }
+    res.eval = rg[0];
+    return res;
+}
+static Affine<HFq2> h_of(const PP* P) { return P ? P->h : Affine<HFq2>{HFq2::zero(), HFq2::zero(), true}; }
+
+static void ser_open(Ser& s, const HFr& eval, const Affine<HFq2>& h, const std::vector<Affine<HFq2>>& proofs) {
     s.fr(eval);
     uint8_t b[96];
-    host::g2_compress(b, P.h);
+    host::g2_compress(b, h);
     s.raw(b, 96);
     s.u64(proofs.size());
     for (auto& p : proofs) {
@@ -757,7 +817,7 @@ static std::vector<HFr> sc1_message(const HFr& Cc, const HFr& tau, const HFr g[3
 }
 
 // ====================================================================== prove
-std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts& o) {
+std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts& o) {
     Timer tall;
     C.timings.clear();
     auto mark = [&](const char* name, Timer& t) {
@@ -775,7 +835,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     const uint64_t nvv = W.v.size() / 32;
     if (!is_pow2(nvv)) invalid("public input should be power of two");
     if (W.n != n) invalid("|v| + |w| != number of variables");  // prover.rs:117-119
-    if (P.nv != L) invalid("public parameter nv != log_n");
+    if (!o.stub && !P) invalid("null public parameter");
+    if (P && P->nv != L) invalid("public parameter nv != log_n");
     const int log_v = ilog2(nvv);
     const Fr* z = W.z.as<Fr>();
     const Fr* zl = z + lo;
@@ -808,7 +869,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     Fr *eqlo = take(8192), *eqhi = take(8192);
     Fr* res3 = take(64);
     Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
-    uint8_t* hp = C.pinned(1 << 16);
+    uint8_t* hp = C.pin_at(Ctx::kPinHp, 1 << 16, 64 << 10);
 
     // ---- SpMV Az, Bz, Cz (challenge-independent: queued first, overlaps the commit's host work)
     {
@@ -819,9 +880,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
         kp_end(I.rows_bytes, C.stream);
     }
     // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
-    commit_launch(C, P, z, n, G, rank);
-    const bool share0 = lvl0_local(L, G);
-    if (share0) lvl0_launch(C, P, zl, L, G, rank);
+    if (!o.stub) commit_launch(C, *P, z, n, G, rank);
+    const bool share0 = !o.stub && lvl0_local(L, G);
+    if (share0) lvl0_launch(C, *P, zl, L, G, rank);
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
@@ -849,7 +910,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
         T.feed(s.b.data(), s.b.size());
     }
     mark("transcript_matrices", tp);
-    Affine<HFq> com = commit_finish(C, G);
+    Affine<HFq> com = o.stub ? Affine<HFq>{HFq::zero(), HFq::zero(), true} : commit_finish(C, G);
     Affine<HFq2> proof0{};
     if (share0) proof0 = lvl0_finish(C, G);
     Ser proof;
@@ -866,9 +927,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = open_z(C, P, zl, L, pt1, G, rank, share0 ? &proof0 : nullptr);
+        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, zl, L, pt1, G, rank, share0 ? &proof0 : nullptr);
         size_t m0 = proof.b.size();
-        ser_open(proof, op.eval, P, op.proofs);
+        ser_open(proof, op.eval, h_of(P), op.proofs);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
     }
     mark("open_rv", tp);
@@ -881,8 +942,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     if (L >= 2)
         launch_eq_table(chdev + 1, L - 1, (uint64_t)rank * (nl / 2), nl / 2, E1, eqlo, eqhi, C.stream);
     else {
-        HFr one = HFr::one();
-        SPX_HIP(hipMemcpyAsync(E1, &one, 32, hipMemcpyHostToDevice, C.stream));
+        const HFr one = HFr::one();
+        memcpy(hp + 4096, &one, 32);
+        SPX_HIP(hipMemcpyAsync(E1, hp + 4096, 32, hipMemcpyHostToDevice, C.stream));
     }
     {
         size_t m0 = proof.b.size();
@@ -1093,8 +1155,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts&
     mark("sumcheck2", tp);
     // ---- round 6: open at r_y (prover.rs:268-281)
     {
-        OpenOut op = open_z(C, P, zl, L, r_y, G, rank, share0 ? &proof0 : nullptr);
-        ser_open(proof, op.eval, P, op.proofs);
+        OpenOut op = o.stub ? open_stub(C, zl, L, r_y, G) : open_z(C, *P, zl, L, r_y, G, rank, share0 ? &proof0 : nullptr);
+        ser_open(proof, op.eval, h_of(P), op.proofs);
     }
     mark("open_ry", tp);
     C.timings.emplace_back("total", tall.us());
@@ -1118,7 +1180,7 @@ VP vp_load(const uint8_t* b, size_t len) {
     };
     uint64_t nv, cnt;
     memcpy(&nv, take(8), 8);
-    if (nv > 40) throw SpxError(kSerialization, "bad verifier parameter nv");
+    if (nv > (uint64_t)kMaxLogN) throw SpxError(kSerialization, "bad verifier parameter nv (<= 26 supported)");
     V.nv = (int)nv;
     if (!host::g1_from_uncompressed(V.g, take(96)) || !host::g2_from_uncompressed(V.h, take(192)))
         throw SpxError(kSerialization, "bad verifier parameter point");
@@ -1293,7 +1355,9 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
     std::vector<HFr> hch(r_x);
     hch.insert(hch.end(), rabc, rabc + 3);
     hch.insert(hch.end(), r_y.begin(), r_y.end());
-    SPX_HIP(hipMemcpyAsync(ch, hch.data(), 32 * hch.size(), hipMemcpyHostToDevice, C.stream));  // pageable: staged
+    uint8_t* hs = C.pin_at(Ctx::kPinStage, 32 * hch.size(), 64 << 10);
+    memcpy(hs, hch.data(), 32 * hch.size());
+    SPX_HIP(hipMemcpyAsync(ch, hs, 32 * hch.size(), hipMemcpyHostToDevice, C.stream));
     launch_eq_table(ch, L, 0, n, EQ, eqlo, eqhi, C.stream);
     SparseView3 cv = I.cols.view();
     launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, ch + L, n, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
@@ -1307,7 +1371,7 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
         launch_open_level(rin, rout, EQ, ch + L + 3 + i, half, C.stream);
         rin = rout;
     }
-    uint8_t* hp = C.pinned(32);
+    uint8_t* hp = C.pin_at(Ctx::kPinOpen, 32, 56 << 10);
     SPX_HIP(hipMemcpyAsync(hp, rin, 32, hipMemcpyDeviceToHost, C.stream));
     C.sync();
     return ld_hfr(hp);
@@ -1437,19 +1501,10 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     if (!is_pow2(n)) invalid("2^(r_x) should have size: num_constraints");
     const int L = ilog2(n);
     // CSC of m (matrices B, C empty), scale (1, 0, 0)
-    const uint64_t nnz = m.rp[n];
-    std::vector<uint64_t> cp(n + 1, 0);
-    for (uint64_t k = 0; k < nnz; ++k) cp[m.col[k] + 1]++;
-    for (uint64_t y = 0; y < n; ++y) cp[y + 1] += cp[y];
-    std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
-    std::vector<uint32_t> rows(nnz);
-    std::vector<uint8_t> vals(32 * nnz);
-    for (uint64_t x = 0; x < n; ++x)
-        for (uint64_t k = m.rp[x]; k < m.rp[x + 1]; ++k) {
-            uint64_t pos = cur[m.col[k]]++;
-            rows[pos] = (uint32_t)x;
-            memcpy(&vals[32 * pos], &m.val[32 * k], 32);
-        }
+    std::vector<uint64_t> cp;
+    std::vector<uint32_t> rows;
+    std::vector<uint8_t> vals;
+    build_csc(m, n, cp, rows, vals);
     std::vector<uint64_t> rps[3] = {cp, std::vector<uint64_t>(n + 1, 0), std::vector<uint64_t>(n + 1, 0)};
     std::vector<uint32_t> cols[3] = {rows, {}, {}};
     std::vector<uint8_t> vv[3] = {vals, {}, {}};
@@ -1540,7 +1595,7 @@ std::vector<uint8_t> k_open(Ctx& C, PP& P, const uint8_t* table, int nv, const u
         if (!host::fr_from_bytes(pt[i], point + 32 * i)) throw SpxError(kSerialization, "non-canonical point");
     OpenOut op = open_z(C, P, W->z.as<Fr>(), nv, pt, 1, 0);
     Ser s;
-    ser_open(s, op.eval, P, op.proofs);
+    ser_open(s, op.eval, P.h, op.proofs);
     return s.b;
 }
 

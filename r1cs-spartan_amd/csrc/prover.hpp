@@ -33,6 +33,10 @@ enum { kOk = 0, kInvalidArgument = 1, kSumcheck = 2, kWrongWitness = 3, kSeriali
 
 inline void invalid(const std::string& m) { throw SpxError(kInvalidArgument, m); }
 
+// Largest supported log_n / nv. Bounded by the MSM references (31-bit point index: n x 16 window
+// copies < 2^31 up to n = 2^26) and by the eq-table scratch (two halves of <= 2^13 entries each).
+static constexpr int kMaxLogN = 26;
+
 // owning device allocation
 struct DevMem {
     void* p = nullptr;
@@ -119,9 +123,20 @@ struct Ctx {
     hipStream_t stream = nullptr;
     MsmWorkspace* msm = nullptr;
     std::unique_ptr<Comm> comm;
-    // pinned staging
+    // Pinned host staging, one fixed carve-out per context (allocated once, never moved: a region a
+    // caller holds stays valid while its async copies run). Every region is reused only after a
+    // stream sync that covers the copies issued from it.
+    enum : size_t {
+        kPinHp = 0,                 // prove(): challenges up, round results down (64 KiB)
+        kPinCommit = 64 << 10,      // commitment MSM result (4 KiB)
+        kPinLvl0 = 68 << 10,        // shared level-0 opening proof (4 KiB)
+        kPinOpen = 72 << 10,        // opening results / evaluations (56 KiB)
+        kPinTailIn = 128 << 10,     // last g opening levels: quotients up (32 KiB)
+        kPinTailOut = 160 << 10,    // ... and their MSM results down (32 KiB)
+        kPinStage = 192 << 10,      // small host-to-device staging (opening points, constants) (64 KiB)
+        kPinBytes = 256 << 10
+    };
     uint8_t* pin = nullptr;
-    size_t pin_bytes = 0;
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
@@ -137,7 +152,8 @@ struct Ctx {
     uint64_t prove_seq = 0;  // proofs started on this context (identical on every rank of its communicator)
     Ctx(int dev);
     ~Ctx();
-    uint8_t* pinned(size_t b);
+    // region [off, off + bytes) of the pinned carve-out (throws if it does not fit its region)
+    uint8_t* pin_at(size_t off, size_t bytes, size_t region);
     void sync() {
         SPX_HIP(hipStreamSynchronize(stream));
         if (kprof.on) kprof.harvest();
@@ -208,6 +224,7 @@ struct ProveOpts {
     int mode = 0;
     uint64_t seed = 0;
     bool cached = false;
+    bool stub = false;  // BASELINE config C2: commitment and opening proofs = identity, no MSM (pp unused)
     // scheduling hooks used by spx_prove_many (neither changes the proof):
     int64_t seq = -1;                 // proof number deciding which rank absorbs A, B, C (default: ctx counter)
     const Blake2s* absorbed = nullptr;  // this proof's A, B, C absorption, already computed by the caller
@@ -224,7 +241,8 @@ std::unique_ptr<PP> pp_generate(Ctx& C, int nv, uint64_t seed);
 std::vector<uint8_t> pp_serialize(Ctx& C, const PP& P);
 std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats);
 std::unique_ptr<Witness> witness_upload(Ctx& C, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw);
-std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP& P, const ProveOpts& o);
+// P may be null only when o.stub
+std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts& o);
 size_t proof_size(int log_n);
 
 // verifier (lib.rs:147-212 with verifier.rs:143-512); VerifierParameter: data_structures.rs:19-26

@@ -6,11 +6,18 @@
 //   kind 1 "ref-shaped": the reference's TestSynthesizer chain circuit
 //          (/root/reference/src/data_structures/constraints.rs:39-110, density 0 by default) padded
 //          square (test_utils.rs:81-102): one dense row of ~n entries in A and B.
+//   kind 3 "circuit-3n": a FIXED index with many satisfying witnesses (the benchmark proves distinct
+//          witnesses of one index). Rows x < n - |v| each define a fresh output variable o_x (a random
+//          permutation of the private columns): A = (alpha, a), B = (beta, b), C = (1, o_x) with a, b
+//          drawn uniformly from the variables defined so far, so z[o_x] = alpha z[a] beta z[b]. The
+//          last |v| rows are (alpha, a) x (1, One) = (alpha, a). The witness seed draws the public
+//          inputs z[1..|v|); every private value follows from them. nnz = 3n; scalars uniform.
 #include "../../include/spartan_hip.h"
 
 #include <algorithm>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host_ff.hpp"
@@ -47,11 +54,71 @@ struct Mat {
 }  // namespace
 
 struct spx_synth {
-    int log_n = 0, log_v = 0;
+    int kind = 0, log_n = 0, log_v = 0;
     uint64_t n = 0;
     Mat m[3];
     std::vector<uint8_t> z;  // canonical bytes
 };
+
+static Fr fr_at(const Mat& M, uint64_t k) {
+    uint64_t c[4];
+    memcpy(c, &M.val[32 * k], 32);
+    return Fr::from_canon(c);
+}
+
+// kind 3: the witness of `wseed` for the circuit in S.m (canonical bytes into out, 32 n)
+static void circuit_witness(const spx_synth& S, uint64_t wseed, uint8_t* out) {
+    const uint64_t n = S.n, nv = 1ull << S.log_v;
+    Sm w{wseed};
+    std::vector<Fr> z(n);
+    z[0] = Fr::one();
+    uint64_t c[4];
+    for (uint64_t i = 1; i < nv; ++i) {
+        do w.fr_canon(c);
+        while (!(c[0] | c[1] | c[2] | c[3]));
+        z[i] = Fr::from_canon(c);
+    }
+    for (uint64_t x = 0; x + nv < n; ++x)
+        z[S.m[2].col[x]] = fr_at(S.m[0], x) * z[S.m[0].col[x]] * fr_at(S.m[1], x) * z[S.m[1].col[x]];
+    for (uint64_t i = 0; i < n; ++i) spx::host::fr_to_bytes(out + 32 * i, z[i]);
+}
+
+static void gen_circuit(spx_synth& S, uint64_t seed, uint64_t wseed) {
+    const uint64_t n = S.n, nv = 1ull << S.log_v;
+    if (nv < 2 || nv >= n) throw std::invalid_argument("circuit-3n needs 2 <= |v| < n");
+    Sm r{seed};
+    std::vector<uint32_t> perm(n - nv);
+    for (uint64_t i = 0; i < n - nv; ++i) perm[i] = (uint32_t)(nv + i);
+    for (uint64_t i = n - nv - 1; i >= 1; --i) std::swap(perm[i], perm[r.next() % (i + 1)]);
+    std::vector<uint32_t> avail;
+    avail.reserve(n);
+    for (uint64_t i = 0; i < nv; ++i) avail.push_back((uint32_t)i);
+    for (int k = 0; k < 3; ++k) {
+        S.m[k].rp.resize(n + 1);
+        S.m[k].col.reserve(n);
+        S.m[k].val.reserve(32 * n);
+        for (uint64_t x = 0; x <= n; ++x) S.m[k].rp[x] = x;
+    }
+    uint64_t c[4];
+    const uint64_t one[4] = {1, 0, 0, 0};
+    for (uint64_t x = 0; x < n; ++x) {
+        const uint32_t a = avail[r.next() % avail.size()];
+        r.fr_canon(c);
+        S.m[0].push(a, c);
+        if (x + nv < n) {
+            const uint32_t b = avail[r.next() % avail.size()];
+            r.fr_canon(c);
+            S.m[1].push(b, c);
+            S.m[2].push(perm[x], one);
+            avail.push_back(perm[x]);
+        } else {
+            S.m[1].push(0, one);
+            S.m[2].push(a, (const uint64_t*)&S.m[0].val[32 * x]);
+        }
+    }
+    S.z.resize(32 * n);
+    circuit_witness(S, wseed, S.z.data());
+}
 
 static void gen_uniform(spx_synth& S, uint64_t seed) {
     const uint64_t n = S.n, mask = n - 1;
@@ -198,11 +265,14 @@ int spx_synth_create(int kind, int log_n, int log_v, uint64_t seed, uint64_t par
         auto S = std::make_unique<spx_synth>();
         S->log_n = log_n;
         S->log_v = log_v;
+        S->kind = kind;
         S->n = 1ull << log_n;
         if (kind == 0)
             gen_uniform(*S, seed);
         else if (kind == 1)
             gen_ref(*S, seed, (int)param);
+        else if (kind == 3)
+            gen_circuit(*S, seed, param);
         else
             return SPX_INVALID_ARGUMENT;
         *out = S.release();
@@ -221,6 +291,17 @@ int spx_synth_csr(const spx_synth* s, int m, spx_csr* out) {
     return SPX_OK;
 }
 const uint8_t* spx_synth_z(const spx_synth* s) { return s->z.data(); }
+int spx_synth_witnesses(const spx_synth* s, uint64_t wseed0, int count, uint8_t* z_out) {
+    if (!s || s->kind != 3 || count < 0 || (count && !z_out)) return SPX_INVALID_ARGUMENT;
+    const int nt = std::max(1, std::min<int>(count, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=] {
+            for (int i = t; i < count; i += nt) circuit_witness(*s, wseed0 + (uint64_t)i, z_out + 32 * s->n * (size_t)i);
+        });
+    for (auto& t : th) t.join();
+    return SPX_OK;
+}
 int spx_synth_free(spx_synth* s) {
     delete s;
     return SPX_OK;

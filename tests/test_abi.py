@@ -36,7 +36,7 @@ def test_proof_size_matches_oracle_layout(spx, oc):
     assert spx.lib().spx_proof_size(20, 5) == 21272  # matches the 2^20 bench proof length
 
 
-@pytest.mark.parametrize("kind,log_n,log_v", [(0, 6, 2), (1, 7, 3), (0, 9, 5)])
+@pytest.mark.parametrize("kind,log_n,log_v", [(0, 6, 2), (1, 7, 3), (0, 9, 5), (3, 6, 2), (3, 10, 5)])
 def test_library_generators_match_oracle(spx, oc, kind, log_n, log_v):
     L = spx.lib()
     L.spx_synth_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
@@ -58,6 +58,23 @@ def test_library_generators_match_oracle(spx, oc, kind, log_n, log_v):
         assert [c.row_ptr[i] for i in range(n + 1)] == [M.row_ptr[i] for i in range(n + 1)]
         assert [c.col[i] for i in range(nnz)] == [M.col[i] for i in range(nnz)]
         assert ctypes.string_at(c.val, 32 * nnz) == M.val.raw[: 32 * nnz]
+    L.spx_synth_free(h)
+
+
+def test_library_circuit_witnesses_match_oracle(spx, oc):
+    """spx_synth_witnesses (kind 3): the witness of every seed equals the oracle generator's."""
+    L = spx.lib()
+    L.spx_synth_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    L.spx_synth_witnesses.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+    L.spx_synth_free.argtypes = [ctypes.c_void_p]
+    log_n, log_v, seed = 8, 3, 4321
+    h = ctypes.c_void_p()
+    assert L.spx_synth_create(3, log_n, log_v, seed, 0, ctypes.byref(h)) == 0
+    n, k = 1 << log_n, 5
+    buf = ctypes.create_string_buffer(32 * n * k)
+    assert L.spx_synth_witnesses(h, 100, k, buf) == 0
+    for i in range(k):
+        assert buf.raw[32 * n * i : 32 * n * (i + 1)] == oc.Instance(3, log_n, log_v, seed, 100 + i).z_bytes
     L.spx_synth_free(h)
 
 

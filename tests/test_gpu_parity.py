@@ -86,6 +86,52 @@ def test_sum_over_y_and_eval_on_x(spx, ctx, oc, kind, log_n, param):
         assert spx.MatrixExtension.eval_on_x(ctx, P, r_x) == oc.eval_on_x(M, r_x)
 
 
+def _with_duplicates(oc, M, seed):
+    """M with repeated columns inside rows: about a third of the rows get one or two extra entries
+    whose column repeats an earlier entry of the same row, with a fresh value, sometimes between
+    other entries. MatrixExtension::new accepts such rows (r1cs_reader.rs:52-60); sum_over_y adds
+    every entry, eval_on_x keeps the last one per (x, y) (r1cs_reader.rs:98-108)."""
+    rs = random.Random(seed)
+    rows = []
+    for row in M.to_rows():
+        row = list(row)
+        if row and rs.random() < 0.35:
+            for _ in range(rs.choice((1, 1, 2))):
+                col = rs.choice(row)[1]
+                row.insert(rs.randrange(len(row) + 1), (rs.randrange(R), col))
+        rows.append(row)
+    return oc.CsrMatrix.from_rows(rows)
+
+
+@pytest.mark.parametrize("kind,log_n,param", [(0, 8, 0), (2, 9, 5 | (2 << 16))])
+def test_sum_over_y_and_eval_on_x_duplicates(spx, ctx, oc, kind, log_n, param):
+    inst = oc.Instance(kind, log_n, 3, 91 + log_n, param)
+    rs = random.Random(7 * log_n)
+    r_x = b"".join(rs.randrange(R).to_bytes(32, "little") for _ in range(log_n))
+    for m, M0 in enumerate(inst.mats):
+        M = _with_duplicates(oc, M0, 1000 * log_n + m)
+        assert M.nnz > M0.nnz
+        P = spx.Csr(M.n, M.row_ptr, M.col, M.val)
+        assert spx.MatrixExtension.sum_over_y(ctx, P, inst.z_bytes) == oc.sum_over_y(M, inst.z_bytes)
+        assert spx.MatrixExtension.eval_on_x(ctx, P, r_x) == oc.eval_on_x(M, r_x)
+
+
+@pytest.mark.parametrize("kind,log_n,log_v", [(0, 6, 2), (2, 9, 3), (0, 11, 5)])
+@pytest.mark.parametrize("mode", ["fs", "injected"])
+def test_prove_bit_exact_duplicates(spx, ctx, oc, kind, log_n, log_v, mode):
+    """Full proofs over matrices with repeated (x, y) entries: the transcript hashes every entry,
+    Az/Bz/Cz sum them, the eval_on_x pass keeps the last one."""
+    param = (3 | (1 << 16)) if kind == 2 else 0
+    inst = oc.Instance(kind, log_n, log_v, 3000 + log_n, param)
+    mats_o = [_with_duplicates(oc, M, 77 * log_n + m) for m, M in enumerate(inst.mats)]
+    ppc = oc.PP.keygen(log_n, 4000 + log_n)
+    pp = spx.PublicParameter.load(ctx, ppc.serialize())
+    pk = spx.MLArgumentForR1CS.index(ctx, *[spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in mats_o])
+    got = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp, mode=mode, seed=66)
+    want = oc.prove(mats_o, inst.v_bytes, inst.w_bytes, ppc, 1 if mode == "injected" else 0, 66)
+    assert got == want
+
+
 @pytest.mark.parametrize("nv", [1, 4, 9])
 def test_commit_open(spx, ctx, oc, nv):
     ppc = oc.PP.keygen(nv, 31 + nv)

@@ -1,7 +1,11 @@
 """Summarise rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE collected in separate runs, as the
 MI355X guide prescribes) into per-kernel HBM bytes per launch.
 
-usage: python tools/pmc_summary.py --fetch DIR --write DIR [--calib DIR] --out profiles/X.json
+usage: python tools/pmc_summary.py --fetch DIR --write DIR [--calib-fetch DIR --calib-write DIR]
+                                  [--valu DIR] --out profiles/X.json
+
+--valu: a pass with SQ_INSTS_VALU (and SQ_WAVES, SQ_INSTS_SALU, SQ_BUSY_CYCLES ...): per-launch VALU
+wave-instructions, the compute side of the MSM kernels' roofline (bench.py).
 
 FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB. On gfx950 FETCH_SIZE counts exactly half
 of the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM section), so fetch bytes are
@@ -16,8 +20,25 @@ import os
 from collections import defaultdict
 
 
-def load(dirname, counter):
-    per = defaultdict(lambda: [0.0, set()])
+def load_all(dirname):
+    """every counter of a pass: {kernel: {counter: (sum, launches)}}"""
+    per = defaultdict(lambda: defaultdict(lambda: [0.0, set()]))
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit("no counter_collection.csv under %s" % dirname)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                rec = per[row["Kernel_Name"]][row["Counter_Name"]]
+                rec[0] += float(row["Counter_Value"])
+                rec[1].add((f, row.get("Dispatch_Id") or row.get("Correlation_Id")))
+    return {k: {c: (v[0], len(v[1])) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def load(dirname, counter, largest=False):
+    """{kernel: (sum of the counter, dispatches)}; largest=True keeps only the dispatches whose value is at
+    least half the kernel's maximum (e.g. the first rounds of a sumcheck, where the tables stream from HBM)"""
+    per = defaultdict(lambda: defaultdict(float))
     files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit("no counter_collection.csv under %s" % dirname)
@@ -26,10 +47,15 @@ def load(dirname, counter):
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
-                k = row["Kernel_Name"]
-                per[k][0] += float(row["Counter_Value"])
-                per[k][1].add((f, row.get("Dispatch_Id") or row.get("Correlation_Id")))
-    return {k: (v[0], len(v[1])) for k, v in per.items()}
+                per[row["Kernel_Name"]][(f, row.get("Dispatch_Id") or row.get("Correlation_Id"))] += float(row["Counter_Value"])
+    out = {}
+    for k, d in per.items():
+        vals = list(d.values())
+        if largest:
+            top = max(vals)
+            vals = [v for v in vals if v >= 0.5 * top]
+        out[k] = (sum(vals), len(vals))
+    return out
 
 
 def short(name):
@@ -42,6 +68,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--calib-fetch")
     ap.add_argument("--calib-write")
+    ap.add_argument("--valu")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     unit = 1024.0  # KiB
@@ -57,6 +84,8 @@ def main():
                  "write_bytes": 1 << 30, "write_reported_bytes": wr[0] / wr[1] * unit, "write_correction": w_corr}
     fe = load(a.fetch, "FETCH_SIZE")
     wr = load(a.write, "WRITE_SIZE")
+    fel = load(a.fetch, "FETCH_SIZE", largest=True)
+    wrl = load(a.write, "WRITE_SIZE", largest=True)
     out = {"unit": "bytes per launch", "fetch_correction": f_corr, "write_correction": w_corr, "calibration": calib,
            "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
@@ -70,7 +99,17 @@ def main():
         }
         if rec["fetch_bytes"] is not None and rec["write_bytes"] is not None:
             rec["traffic_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
+        lf, lw = fel.get(k), wrl.get(k)
+        if lf and lw and lf[1] and lw[1]:
+            rec["traffic_bytes_largest"] = lf[0] / lf[1] * unit * f_corr + lw[0] / lw[1] * unit * w_corr
         out["kernels"][short(k)] = rec
+    if a.valu:
+        out["valu_counters"] = "SQ_* per launch (SQ_INSTS_VALU = VALU wave-instructions)"
+        for k, cs in load_all(a.valu).items():
+            rec = out["kernels"].setdefault(short(k), {})
+            for c, (tot, n) in cs.items():
+                rec[c + "_per_launch"] = tot / n if n else None
+                rec["launches_valu_pass"] = n
     json.dump(out, open(a.out, "w"), indent=1)
     print("wrote", a.out, len(out["kernels"]), "kernels")
 

@@ -106,6 +106,12 @@ def synth_instance(spx, kind, log_n, log_v, seed, n_wit, wseed0):
     return h, mats, zs, nnz
 
 
+def synth_one(spx, kind, log_n, log_v, seed):
+    """(handle, CSR views, z bytes, nnz) of one generated instance (tests)"""
+    h, mats, zs, nnz = synth_instance(spx, kind, log_n, log_v, seed, 1, 0xB0B0)
+    return h, mats, zs[0], nnz
+
+
 def index_from_c(spx, ctx, mats):
     h = ctypes.c_void_p()
     a, b, c = mats

@@ -92,6 +92,9 @@ int spx_comm_shm_destroy(void *comm);
 int spx_comm_group_create(int world, void **group_out);
 int spx_comm_group_destroy(void *group);
 int spx_ctx_set_comm_group(spx_ctx *ctx, void *group, int rank);
+/* one allgather on the context's communicator (whatever its transport): every rank passes `bytes`,
+ * recv receives world * bytes in rank order. For transport tests. */
+int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t bytes);
 
 /* ---- public parameters ---- */
 int spx_pp_load(spx_ctx *ctx, const uint8_t *bytes, size_t len, spx_pp **out);

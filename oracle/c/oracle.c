@@ -1092,6 +1092,64 @@ void orc_eval_on_x(const orc_csr *M, const uint8_t *r_x, uint8_t *out) {
     for (uint64_t i = 0; i < M->n; ++i) fr_to_bytes(out + 32 * i, &o[i]);
     free(o), free(r), free(m.val);
 }
+/* M(r_x, r_y) = sum over the entries of M of a eq(r_x, x) eq(r_y, y), where a row that repeats a
+ * column contributes its last entry for it (eval_on_x's map insert, r1cs_reader.rs:98-108): the
+ * verifier's final matrix claim (verifier.rs:493-495) in O(nnz), for full-size replays */
+void orc_matrix_eval(const orc_csr *M, const uint8_t *r_x, const uint8_t *r_y, uint8_t *out) {
+    uint64_t n = M->n;
+    int s = ark_log2(n);
+    fr_t *rx = frs_from_bytes(r_x, (size_t)s), *ry = frs_from_bytes(r_y, (size_t)s);
+    fr_t *ex = (fr_t *)malloc(sizeof(fr_t) * n), *ey = (fr_t *)malloc(sizeof(fr_t) * n);
+    eq_table(ex, rx, s);
+    eq_table(ey, ry, s);
+    uint64_t *last_row = (uint64_t *)malloc(8 * n), *last_k = (uint64_t *)malloc(8 * n);
+    for (uint64_t y = 0; y < n; ++y) last_row[y] = ~0ULL;
+    fr_t acc, t, v;
+    fr_zero(&acc);
+    for (uint64_t x = 0; x < n; ++x) {
+        for (uint64_t k = M->row_ptr[x]; k < M->row_ptr[x + 1]; ++k) last_row[M->col[k]] = x, last_k[M->col[k]] = k;
+        fr_t row;
+        fr_zero(&row);
+        for (uint64_t k = M->row_ptr[x]; k < M->row_ptr[x + 1]; ++k) {
+            uint32_t y = M->col[k];
+            if (last_k[y] != k) continue; /* superseded by a later entry of this row */
+            fr_from_bytes(&v, M->val + 32 * k);
+            fr_mul(&t, &v, &ey[y]);
+            fr_add(&row, &row, &t);
+        }
+        fr_mul(&t, &row, &ex[x]);
+        fr_add(&acc, &acc, &t);
+    }
+    fr_to_bytes(out, &acc);
+    free(rx), free(ry), free(ex), free(ey), free(last_row), free(last_k);
+}
+
+/* mKZG opening checked against the keygen trapdoor t (open.rs:37-49 + setup.rs:37-60): for every level
+ * i, q_i = r[2b+1] - r[2b] of the folded table, qv[i] = q_i(t[i+1..nv]) (pi_i = h^{qv[i]}), and the
+ * final evaluation z(point) */
+void orc_open_trapdoor(const uint8_t *table, int nv, const uint8_t *point, const uint8_t *t_bytes, uint8_t *qv_out,
+                       uint8_t *eval_out) {
+    size_t n = (size_t)1 << nv;
+    fr_t *r = frs_from_bytes(table, n), *pt = frs_from_bytes(point, (size_t)nv), *t = frs_from_bytes(t_bytes, (size_t)nv);
+    fr_t *q = (fr_t *)malloc(sizeof(fr_t) * (n / 2 + 1));
+    for (int i = 0; i < nv; ++i) {
+        size_t h = (size_t)1 << (nv - i - 1);
+        for (size_t b = 0; b < h; ++b) fr_sub(&q[b], &r[2 * b + 1], &r[2 * b]);
+        fr_t qv;
+        mle_eval(&qv, q, nv - i - 1, t + i + 1);
+        fr_to_bytes(qv_out + 32 * i, &qv);
+        fix_first(r, 2 * h, &pt[i]);
+    }
+    fr_to_bytes(eval_out, &r[0]);
+    free(r), free(pt), free(t), free(q);
+}
+/* z(t) (the commitment is g^{z(t)}, commit.rs:53-66) */
+void orc_mle_eval(const uint8_t *table, int nv, const uint8_t *point, uint8_t *out) {
+    fr_t *z = frs_from_bytes(table, (size_t)1 << nv), *pt = frs_from_bytes(point, (size_t)nv), ev;
+    mle_eval(&ev, z, nv, pt);
+    fr_to_bytes(out, &ev);
+    free(z), free(pt);
+}
 void orc_msm_g1(const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out) {
     g1_aff *b = (g1_aff *)malloc(sizeof(g1_aff) * (n ? n : 1));
     uint64_t(*sc)[4] = malloc(32 * (n ? n : 1));

@@ -54,6 +54,12 @@ void orc_commit(const orc_pp *pp, const uint8_t *table, int nv, uint8_t *out56);
 void orc_open(const orc_pp *pp, const uint8_t *table, int nv, const uint8_t *point, uint8_t *eval_out,
               uint8_t *proof_out);
 
+/* ---- full-size checkers (tests): final matrix claim, openings against the keygen trapdoor ---- */
+void orc_matrix_eval(const orc_csr *M, const uint8_t *r_x, const uint8_t *r_y, uint8_t *out);
+void orc_open_trapdoor(const uint8_t *table, int nv, const uint8_t *point, const uint8_t *t, uint8_t *qv_out,
+                       uint8_t *eval_out);
+void orc_mle_eval(const uint8_t *table, int nv, const uint8_t *point, uint8_t *out);
+
 /* ---- full argument (lib.rs:58-146) ----
  * mode 0 = Fiat-Shamir (Blake2s512Rng transcript), 1 = injected challenges (SplitMix64(inj_seed));
  * OR 2 = commitment stubbed (BASELINE config C2: identity commitment and opening proofs, no MSM,

@@ -68,6 +68,10 @@ def lib():
             ctypes.c_size_t,
             ctypes.POINTER(ctypes.c_size_t),
         ]
+        L.orc_matrix_eval.argtypes = [ctypes.POINTER(Csr), ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+        L.orc_open_trapdoor.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_mle_eval.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -250,3 +254,29 @@ def prove(mats, v_bytes, w_bytes, pp, mode=0, inj_seed=0, commitment_stub=False)
     if rc:
         raise RuntimeError("orc_prove failed (%d): %s" % (rc, L.orc_last_error().decode()))
     return out.raw[: ln.value]
+
+
+def _frb(xs):
+    return b"".join(int(x).to_bytes(32, "little") for x in xs)
+
+
+def matrix_eval(M, r_x, r_y):
+    """M(r_x, r_y) with eval_on_x's last-entry semantics; M a CsrMatrix or a ctypes Csr view"""
+    out = ctypes.create_string_buffer(32)
+    c = M.csr() if hasattr(M, "csr") else M
+    lib().orc_matrix_eval(ctypes.byref(c), _frb(r_x), _frb(r_y), out)
+    return int.from_bytes(out.raw, "little")
+
+
+def open_trapdoor(table_bytes, nv, point, t):
+    """([q_i(t[i+1..])] for every level, z(point)) of an mKZG opening"""
+    qv = ctypes.create_string_buffer(32 * max(nv, 1))
+    ev = ctypes.create_string_buffer(32)
+    lib().orc_open_trapdoor(table_bytes, nv, _frb(point), _frb(t), qv, ev)
+    return [int.from_bytes(qv.raw[32 * i : 32 * i + 32], "little") for i in range(nv)], int.from_bytes(ev.raw, "little")
+
+
+def mle_eval(table_bytes, nv, point):
+    out = ctypes.create_string_buffer(32)
+    lib().orc_mle_eval(table_bytes, nv, _frb(point), out)
+    return int.from_bytes(out.raw, "little")

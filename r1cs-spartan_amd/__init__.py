@@ -82,6 +82,7 @@ EXPORTED = [
     "spx_comm_group_create",
     "spx_comm_group_destroy",
     "spx_ctx_set_comm_group",
+    "spx_ctx_comm_allgather",
     "spx_pp_load",
     "spx_pp_generate",
     "spx_pp_serialize",
@@ -142,6 +143,7 @@ def lib():
     L.spx_comm_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
+    L.spx_ctx_comm_allgather.argtypes = [vp, ctypes.c_char_p, ctypes.c_void_p, sz]
     L.spx_pp_load.argtypes = [vp, u8p, sz, ctypes.POINTER(vp)]
     L.spx_pp_generate.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
     L.spx_pp_serialize.argtypes = [vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
@@ -262,6 +264,13 @@ class Context:
 
     def set_comm_group(self, group, rank):
         _check(lib().spx_ctx_set_comm_group(self.h, group.h, int(rank)))
+
+    def comm_allgather(self, data, world):
+        """one allgather of `data` on this context's communicator -> list of world byte strings"""
+        data = bytes(data)
+        out = ctypes.create_string_buffer(max(1, len(data) * world))
+        _check(lib().spx_ctx_comm_allgather(self.h, data, out, len(data)))
+        return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(world)]
 
     def last_timings(self):
         buf = (ctypes.c_double * 32)()

@@ -164,6 +164,14 @@ int spx_ctx_set_comm_group(spx_ctx* ctx, void* group, int rank) {
     });
 }
 
+int spx_ctx_comm_allgather(spx_ctx* ctx, const void* send, void* recv, size_t bytes) {
+    return guard([&] {
+        set_dev(ctx);
+        if (bytes && (!send || !recv)) spx::invalid("null argument");
+        ctx->c->comm->allgather(send, recv, bytes);
+    });
+}
+
 int spx_pp_load(spx_ctx* ctx, const uint8_t* bytes, size_t len, spx_pp** out) {
     return guard([&] {
         set_dev(ctx);

@@ -56,7 +56,7 @@ def main():
     ctxs = [spx.Context(0) for _ in range(a.inflight)]
     for k, c in enumerate(ctxs):
         c.set_comm_shm("%s_%d" % (a.name, k), a.rank, a.world)
-    syn, mats, z, nnz = bench.synth_instance(spx, 0, a.log_n, a.log_v, 0x5EED0000 + a.log_n)
+    syn, mats, z, nnz = bench.synth_one(spx, 0, a.log_n, a.log_v, 0x5EED0000 + a.log_n)
     pp = spx.MLProofForR1CS.setup(ctxs[0], a.log_n, 77)
     pk = spx.IndexPK(ctxs[0], bench.index_from_c(spx, ctxs[0], mats), a.log_n)
     wit = spx.Witness(ctxs[0], z[: 32 << a.log_v], z[32 << a.log_v :])

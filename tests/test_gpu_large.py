@@ -1,8 +1,10 @@
 """BASELINE configs C4 / C5 at their sizes on one GPU: 2^22 and 2^24 constraints (uniform-3n,
 nnz = 3n), the proof sharded over 8 ranks (8 contexts with an in-process communicator on the one
 GPU: the bench's N = 8 decomposition and exchanges, minus the transport) must equal the unsharded
-proof byte for byte, and the product's verifier must accept it (the CPU oracle cannot prove at these
-sizes; the 2^20 test checks the verifier itself against the oracle's replay and the trapdoor)."""
+proof byte for byte, the product's verifier must accept it, and the proof must pass the oracle's
+complete transcript replay (every sumcheck relation, the final matrix claim from the CSR) and the
+commitment / opening checks against the keygen trapdoor (tests/fullsize_check.py): the CPU oracle
+cannot prove at these sizes, so the sharded GPU proof is checked instead of compared."""
 import os
 import sys
 import threading
@@ -14,12 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("log_n", [22, 24])
-def test_sharded_8_ranks_large(spx, ctx, log_n):
+def test_sharded_8_ranks_large(spx, ctx, oc, log_n):
     sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import bench
+    from fullsize_check import replay_and_trapdoor
 
     log_v, G = 5, 8
-    syn, mats, zb, nnz = bench.synth_instance(spx, 0, log_n, log_v, 0x5EED0000 + log_n)
+    syn, mats, zb, nnz = bench.synth_one(spx, 0, log_n, log_v, 0x5EED0000 + log_n)
     assert nnz == 3 << log_n
     v, w = zb[: 32 << log_v], zb[32 << log_v :]
     pp = spx.MLProofForR1CS.setup(ctx, log_n, 0xC0FFEE)
@@ -51,3 +55,4 @@ def test_sharded_8_ranks_large(spx, ctx, log_n):
     assert not errs, errs
     for r in range(G):
         assert out[r] == want, "rank %d proof differs" % r
+    replay_and_trapdoor(oc, mats, zb, want, log_n, log_v, 0xC0FFEE)

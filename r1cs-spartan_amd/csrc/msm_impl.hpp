@@ -2,9 +2,63 @@
 // so the heavy big-integer code of G1 and G2 compiles in parallel.
 #pragma once
 #include "curve29.hpp"
+#include "fq2pair.hpp"
 #include "msm_common.hpp"
 
 namespace spx {
+
+// Representation of the accumulation / weighting kernels per curve: G1 runs one point per lane
+// (radix-2^29 Fq), G2 one point per lane PAIR (fq2pair.hpp: c0 on the even lane, c1 on the odd),
+// so a G2 lane holds half a point and two waves fit each SIMD.
+template <class F>
+struct Acc;
+template <>
+struct Acc<Fq> {
+    using T = F29;
+    static constexpr int kLanes = 1, kWaves = 1;
+    static DEV void ld_aff(T& x, T& y, const Aff<Fq>* p) {
+        Aff<Fq> a;
+        load_vec(a, p);
+        f29_unpack(x, a.x.v);
+        f29_unpack(y, a.y.v);
+    }
+    static DEV bool aff_sentinel(const T& x, const T& y) { return f29_is_zero_raw(x) && f29_is_zero_raw(y); }
+    static DEV void ld(X29<T>& r, const Xyzz<Fq>* p) { ld29<Fq>(r, p); }
+    static DEV void st(Xyzz<Fq>* p, const X29<T>& r) { st29<Fq>(p, r); }
+};
+template <>
+struct Acc<Fq2> {
+    using T = FP29;
+    static constexpr int kLanes = 2, kWaves = 2;
+    static DEV void ld_aff(T& x, T& y, const Aff<Fq2>* p) {
+        fp29_ld(x, &p->x);
+        fp29_ld(y, &p->y);
+    }
+    static DEV bool aff_sentinel(const T& x, const T& y) {
+        return pair_all(f29_is_zero_raw(x.v) && f29_is_zero_raw(y.v));
+    }
+    static DEV void ld(X29<T>& r, const Xyzz<Fq2>* p) {
+        fp29_ld(r.x, &p->x);
+        fp29_ld(r.y, &p->y);
+        fp29_ld(r.zz, &p->zz);
+        fp29_ld(r.zzz, &p->zzz);
+    }
+    static DEV void st(Xyzz<Fq2>* p, const X29<T>& r) {
+        fp29_st(&p->x, r.x);
+        fp29_st(&p->y, r.y);
+        fp29_st(&p->zz, r.zz);
+        fp29_st(&p->zzz, r.zzz);
+    }
+};
+// element index of the calling lane (one element per Acc<F>::kLanes lanes)
+template <class F>
+DEV uint64_t acc_elem() {
+    return (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / Acc<F>::kLanes;
+}
+template <class F>
+static unsigned acc_blocks(uint64_t elems) {
+    return (unsigned)((elems * Acc<F>::kLanes + kHeavy - 1) / kHeavy);
+}
 
 // ------------------------------------------------------------------ accumulation levels
 // Accumulation and weighting run in the radix-2^29 domain (ff29.hpp / curve29.hpp): tables and
@@ -14,13 +68,14 @@ namespace spx {
 // crosses into the next (non-empty) bucket stores the finished partial and restarts; bucket b's
 // partials are pfx[b] + (t - off[b] / seg1) for the threads t its range intersects.
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict__ off, uint32_t nb,
-                                                      const uint32_t* __restrict__ pfx,
-                                                      const uint32_t* __restrict__ refs,
-                                                      const Aff<F>* __restrict__ pts, Xyzz<F>* __restrict__ out,
-                                                      uint32_t seg1) {
-    using T = typename R29<F>::T;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint32_t* __restrict__ off, uint32_t nb,
+                                                                      const uint32_t* __restrict__ pfx,
+                                                                      const uint32_t* __restrict__ refs,
+                                                                      const Aff<F>* __restrict__ pts,
+                                                                      Xyzz<F>* __restrict__ out, uint32_t seg1) {
+    using A = Acc<F>;
+    using T = typename A::T;
+    const uint32_t t = (uint32_t)acc_elem<F>();
     const uint32_t total = off[nb];
     uint32_t e = t * seg1;
     if (e >= total) return;
@@ -32,7 +87,7 @@ __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict
     x29_set_inf(acc);
     for (; e < end; ++e) {
         if (e == bend) {  // bucket b is finished inside this range: the next one starts here
-            st29<F>(out + slot, acc);
+            A::st(out + slot, acc);
             x29_set_inf(acc);
             do {
                 ++b;
@@ -43,37 +98,36 @@ __global__ __launch_bounds__(kHeavy) void k_accum_aff(const uint32_t* __restrict
         // (a software-pipelined variant that issues the next point's load before this addition
         // measured 2.5% slower end to end: more AGPR traffic at occupancy 1)
         const uint32_t r = refs[e];
-        Aff<F> p;
-        load_vec(p, pts + (r & 0x7fffffffu));
-        if (aff_is_sentinel(p)) continue;
         T px, py;
-        R29<F>::unpack(px, p.x);
-        R29<F>::unpack(py, p.y);
+        A::ld_aff(px, py, pts + (r & 0x7fffffffu));
+        if (A::aff_sentinel(px, py)) continue;
         x29_madd(acc, px, py, (r >> 31) != 0);
     }
-    st29<F>(out + slot, acc);
+    A::st(out + slot, acc);
 }
 
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restrict__ segoff, uint32_t nb,
-                                                       const uint32_t* __restrict__ off,
-                                                       const uint32_t* __restrict__ cnt,
-                                                       const Xyzz<F>* __restrict__ in, Xyzz<F>* __restrict__ out) {
-    using T = typename R29<F>::T;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uint32_t* __restrict__ segoff, uint32_t nb,
+                                                                       const uint32_t* __restrict__ off,
+                                                                       const uint32_t* __restrict__ cnt,
+                                                                       const Xyzz<F>* __restrict__ in,
+                                                                       Xyzz<F>* __restrict__ out) {
+    using A = Acc<F>;
+    using T = typename A::T;
+    const uint32_t s = (uint32_t)acc_elem<F>();
     if (s >= segoff[nb]) return;
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
     const uint32_t start = off[b] + k * kSeg;
     const uint32_t end = min(start + kSeg, off[b] + cnt[b]);
     X29<T> acc;
-    ld29<F>(acc, in + start);
+    A::ld(acc, in + start);
     for (uint32_t e = start + 1; e < end; ++e) {
         X29<T> p;
-        ld29<F>(p, in + e);
+        A::ld(p, in + e);
         x29_add(acc, p);
     }
-    st29<F>(out + s, acc);
+    A::st(out + s, acc);
 }
 
 // ------------------------------------------------------------------ bucket weighting: chunks + tree
@@ -92,12 +146,12 @@ __global__ __launch_bounds__(kHeavy) void k_accum_xyzz(const uint32_t* __restric
 DEV uint32_t tree_chunk_log(uint32_t c) { return c - 2 < kTreeChunkLog ? c - 2 : kTreeChunkLog; }
 
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_tree_chunk(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp,
-                                                       int ninst, const uint32_t* __restrict__ node_off,
-                                                       const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                                       const Xyzz<F>* __restrict__ P, Xyzz<F>* __restrict__ Fo,
-                                                       Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
+    const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp, int ninst, const uint32_t* __restrict__ node_off,
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, const Xyzz<F>* __restrict__ P,
+    Xyzz<F>* __restrict__ Fo, Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
+    using A = Acc<F>;
+    const uint64_t t = acc_elem<F>();
     if (t >= wp[ninst]) return;
     const int i = find_slot(wp, ninst, t);
     const uint32_t k = (uint32_t)(t - wp[i]);
@@ -107,7 +161,7 @@ __global__ __launch_bounds__(kHeavy) void k_tree_chunk(const MsmInst* __restrict
     const uint32_t o = node_off[i] + k;
     // F accumulates in its output slot, and both kinds of step (run += X_j, F += run) go through one
     // addition site with two points live: a G2 XYZZ point is 112 registers in radix 2^29
-    using T = typename R29<F>::T;
+    using T = typename A::T;
     X29<T> run;
     x29_set_inf(run);
     const int m = 1 << lgm;
@@ -119,37 +173,36 @@ __global__ __launch_bounds__(kHeavy) void k_tree_chunk(const MsmInst* __restrict
         if (bucket_step) {
             if (!cnt[b0 + j]) continue;
             a = run;
-            ld29<F>(b, P + off[b0 + j]);
+            A::ld(b, P + off[b0 + j]);
         } else {
             if (j == m - 1) {  // F = run for the top bucket
-                st29<F>(Fo + o, run);
+                A::st(Fo + o, run);
                 continue;
             }
-            ld29<F>(a, Fo + o);
+            A::ld(a, Fo + o);
             b = run;
         }
         x29_add(a, b);
         if (bucket_step) {
             run = a;
         } else {
-            st29<F>(Fo + o, a);
+            A::st(Fo + o, a);
             run = b;
         }
     }
-    st29<F>(So + o, run);
+    A::st(So + o, run);
 #pragma unroll 1
     for (uint32_t d = 0; d < lgm; ++d) x29_dbl(run);
-    st29<F>(Do + o, run);
+    A::st(Do + o, run);
 }
 
 template <class F>
-__global__ __launch_bounds__(kHeavy) void k_tree_level(const uint64_t* __restrict__ wp, int ninst,
-                                                       const uint32_t* __restrict__ node_off,
-                                                       const uint32_t* __restrict__ cnt_in,
-                                                       const Xyzz<F>* __restrict__ Fi, const Xyzz<F>* __restrict__ Si,
-                                                       const Xyzz<F>* __restrict__ Di, Xyzz<F>* __restrict__ Fo,
-                                                       Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
+    const uint64_t* __restrict__ wp, int ninst, const uint32_t* __restrict__ node_off, const uint32_t* __restrict__ cnt_in,
+    const Xyzz<F>* __restrict__ Fi, const Xyzz<F>* __restrict__ Si, const Xyzz<F>* __restrict__ Di,
+    Xyzz<F>* __restrict__ Fo, Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
+    using A = Acc<F>;
+    const uint64_t t = acc_elem<F>();
     const uint64_t N = wp[ninst];
     if (t >= 3 * N) return;
     const uint32_t comp = (uint32_t)(t / N);
@@ -158,31 +211,31 @@ __global__ __launch_bounds__(kHeavy) void k_tree_level(const uint64_t* __restric
     const uint32_t k = (uint32_t)(tn - wp[i]);
     const uint32_t base = node_off[i], n = cnt_in[i];
     const bool has_r = 2 * k + 1 < n;
-    X29<typename R29<F>::T> a, b;
+    X29<typename A::T> a, b;
     if (comp == 0) {  // F_l + D_r + F_r
-        ld29<F>(a, Fi + base + 2 * k);
+        A::ld(a, Fi + base + 2 * k);
         if (has_r) {
-            ld29<F>(b, Di + base + 2 * k + 1);
+            A::ld(b, Di + base + 2 * k + 1);
             x29_add(a, b);
-            ld29<F>(b, Fi + base + 2 * k + 1);
+            A::ld(b, Fi + base + 2 * k + 1);
             x29_add(a, b);
         }
-        st29<F>(Fo + base + k, a);
+        A::st(Fo + base + k, a);
     } else if (comp == 1) {
-        ld29<F>(a, Si + base + 2 * k);
+        A::ld(a, Si + base + 2 * k);
         if (has_r) {
-            ld29<F>(b, Si + base + 2 * k + 1);
+            A::ld(b, Si + base + 2 * k + 1);
             x29_add(a, b);
         }
-        st29<F>(So + base + k, a);
+        A::st(So + base + k, a);
     } else {
-        ld29<F>(a, Di + base + 2 * k);
+        A::ld(a, Di + base + 2 * k);
         if (has_r) {
-            ld29<F>(b, Di + base + 2 * k + 1);
+            A::ld(b, Di + base + 2 * k + 1);
             x29_add(a, b);
         }
         x29_dbl(a);
-        st29<F>(Do + base + k, a);
+        A::st(Do + base + k, a);
     }
 }
 
@@ -220,8 +273,8 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     exclusive_scan(ws, so.segcnt, so.soa, nb + 1, s);
     const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
-    hipLaunchKernelGGL(k_accum_aff<F>, dim3((unsigned)((nthr + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s, so.offs, nb,
-                       so.soa, so.refs, pts, PA, kSeg1);
+    hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, so.soa, so.refs, pts, PA,
+                       kSeg1);
     // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
     kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s, (double)tot_refs);
     uint32_t* cur_cnt = so.segcnt;
@@ -237,8 +290,8 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
         exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
-        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3((unsigned)((nsegs + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
-                           nxt_off, nb, cur_off, cur_cnt, cur, nxt);
+        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(acc_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur_cnt,
+                           cur, nxt);
         kp_end((double)(cur_max_segs + nsegs) * psz, s, (double)cur_max_segs);
         std::swap(cur, nxt);
         std::swap(cur_off, nxt_off);
@@ -289,14 +342,13 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     {
         uint64_t work = wp[ninst];
-        hipLaunchKernelGGL(k_tree_chunk<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
-                           so.d_insts, d_wp, ninst, d_noff, cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
+        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(acc_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, ninst, d_noff,
+                           cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
     }
     for (int lv = 1; lv <= levels; ++lv) {
         uint64_t work = 3 * wp[(size_t)lv * (ninst + 1) + ninst];
-        hipLaunchKernelGGL(k_tree_level<F>, dim3((unsigned)((work + kHeavy - 1) / kHeavy)), dim3(kHeavy), 0, s,
-                           d_wp + (size_t)lv * (ninst + 1), ninst, d_noff, d_cin + (size_t)lv * ninst, A3[0], A3[1],
-                           A3[2], B3[0], B3[1], B3[2]);
+        hipLaunchKernelGGL(k_tree_level<F>, dim3(acc_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (ninst + 1),
+                           ninst, d_noff, d_cin + (size_t)lv * ninst, A3[0], A3[1], A3[2], B3[0], B3[1], B3[2]);
         std::swap(A3, B3);
     }
     hipLaunchKernelGGL(k_tree_out<F>, dim3((ninst + 63) / 64), dim3(64), 0, s, ninst, d_noff, A3[0], (Xyzz<F>*)out_dev);

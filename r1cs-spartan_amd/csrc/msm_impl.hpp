@@ -12,15 +12,32 @@ namespace spx {
 // so a G2 lane holds half a point and two waves fit each SIMD.
 template <class F>
 struct Acc;
+#ifndef SPX_G1_WAVES
+#define SPX_G1_WAVES 1
+#endif
+#ifndef SPX_G2_WAVES
+#define SPX_G2_WAVES 2
+#endif
+#ifndef SPX_ACC_PREFETCH
+#define SPX_ACC_PREFETCH 0
+#endif
+// one lane's packed affine coordinates (G1: the point; G2: its half), as loaded from the table
+struct AffRaw {
+    Fq x, y;
+};
 template <>
 struct Acc<Fq> {
     using T = F29;
-    static constexpr int kLanes = 1, kWaves = 1;
-    static DEV void ld_aff(T& x, T& y, const Aff<Fq>* p) {
-        Aff<Fq> a;
-        load_vec(a, p);
+    static constexpr int kLanes = 1, kWaves = SPX_G1_WAVES;
+    static DEV void ld_raw(AffRaw& a, const Aff<Fq>* p) { load_vec(*(Aff<Fq>*)&a, p); }
+    static DEV void unpack(T& x, T& y, const AffRaw& a) {
         f29_unpack(x, a.x.v);
         f29_unpack(y, a.y.v);
+    }
+    static DEV void ld_aff(T& x, T& y, const Aff<Fq>* p) {
+        AffRaw a;
+        ld_raw(a, p);
+        unpack(x, y, a);
     }
     static DEV bool aff_sentinel(const T& x, const T& y) { return f29_is_zero_raw(x) && f29_is_zero_raw(y); }
     static DEV void ld(X29<T>& r, const Xyzz<Fq>* p) { ld29<Fq>(r, p); }
@@ -29,7 +46,16 @@ struct Acc<Fq> {
 template <>
 struct Acc<Fq2> {
     using T = FP29;
-    static constexpr int kLanes = 2, kWaves = 2;
+    static constexpr int kLanes = 2, kWaves = SPX_G2_WAVES;
+    static DEV void ld_raw(AffRaw& a, const Aff<Fq2>* p) {
+        const bool odd = pair_odd();
+        load_vec(a.x, odd ? &p->x.c1 : &p->x.c0);
+        load_vec(a.y, odd ? &p->y.c1 : &p->y.c0);
+    }
+    static DEV void unpack(T& x, T& y, const AffRaw& a) {
+        f29_unpack(x.v, a.x.v);
+        f29_unpack(y.v, a.y.v);
+    }
     static DEV void ld_aff(T& x, T& y, const Aff<Fq2>* p) {
         fp29_ld(x, &p->x);
         fp29_ld(y, &p->y);
@@ -85,6 +111,11 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
     uint32_t slot = pfx[b] + (t - off[b] / seg1);
     X29<T> acc;
     x29_set_inf(acc);
+#if SPX_ACC_PREFETCH
+    uint32_t rn = refs[e];
+    AffRaw nxt;
+    A::ld_raw(nxt, pts + (rn & 0x7fffffffu));
+#endif
     for (; e < end; ++e) {
         if (e == bend) {  // bucket b is finished inside this range: the next one starts here
             A::st(out + slot, acc);
@@ -97,9 +128,21 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
         }
         // (a software-pipelined variant that issues the next point's load before this addition
         // measured 2.5% slower end to end: more AGPR traffic at occupancy 1)
+#if SPX_ACC_PREFETCH
+        // the next reference's point is loaded before this addition (its latency hides behind it)
+        const uint32_t r = rn;
+        const AffRaw cur = nxt;
+        if (e + 1 < end) {
+            rn = refs[e + 1];
+            A::ld_raw(nxt, pts + (rn & 0x7fffffffu));
+        }
+        T px, py;
+        A::unpack(px, py, cur);
+#else
         const uint32_t r = refs[e];
         T px, py;
         A::ld_aff(px, py, pts + (r & 0x7fffffffu));
+#endif
         if (A::aff_sentinel(px, py)) continue;
         x29_madd(acc, px, py, (r >> 31) != 0);
     }

@@ -109,6 +109,11 @@ int main() {
     printf("shader clock (one wave, idle chip): %.0f MHz\n", fclk / 1e6);
     if (fclk < 1.0e9 || fclk > 3.0e9) fclk = 2.4e9;
     fclk = 2.4e9;  // price against the spec clock (MI355X_MICROARCH.md: 2400 MHz)
+    run<0, 1, 1>("v_mad_u64_u32", buf, fclk);  // one dependent chain: latency
+    run<0, 2, 1>("v_mad_u64_u32", buf, fclk);
+    run<0, 4, 1>("v_mad_u64_u32", buf, fclk);
+    run<0, 1, 2>("v_mad_u64_u32", buf, fclk);
+    run<0, 2, 2>("v_mad_u64_u32", buf, fclk);
     run<0, 1, 16>("v_mad_u64_u32", buf, fclk);
     run<0, 1, 32>("v_mad_u64_u32", buf, fclk);
     run<1, 1, 16>("v_add_u32", buf, fclk);

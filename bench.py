@@ -512,7 +512,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
         "higher_is_better": True,
-        "scaling": "strong" if sharded_head else "weak",
+        # --shard proof (default): the same proofs split over however many ranks (N = 1 included)
+        "scaling": "strong" if (sharded_head or (world == 1 and args.shard == "proof")) else "weak",
         "vs_baseline": None,
         "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
         "data": "synthetic",

@@ -14,8 +14,14 @@ namespace spx {
 
 static constexpr uint32_t kSeg1Default = 32;  // references per thread, affine accumulation level
 uint32_t seg1_len(bool g2);                      // kSeg1Default unless SPX_KSEG1 / SPX_KSEG1_G2 (tuning)
-static constexpr uint32_t kSeg = 32;    // partials per thread, XYZZ accumulation levels
-static constexpr uint32_t kTreeChunkLog = 4;  // buckets per running-sum chunk of the weighting leaf: 16
+#ifndef SPX_XYZZ_SEG
+#define SPX_XYZZ_SEG 4
+#endif
+static constexpr uint32_t kSeg = SPX_XYZZ_SEG;  // partials per thread, XYZZ accumulation levels (4: shallow levels)
+#ifndef SPX_TREE_CHUNK_LOG
+#define SPX_TREE_CHUNK_LOG 2
+#endif
+static constexpr uint32_t kTreeChunkLog = SPX_TREE_CHUNK_LOG;  // buckets per running-sum chunk of the weighting leaf: 4
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
 

@@ -299,15 +299,45 @@ __global__ void k_points_from_bytes(Fq* pts, uint64_t n, int* err) {
             for (int k = 0; k < NF; ++k) store_vec(p + k, z);
             continue;
         }
+        Fq m[NF];
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
-            Fq c, m;
+            Fq c;
             load_vec(c, p + k);
             if (k == NF - 1) c.v[11] &= 0x3fffffffu;
-            ok &= fq_canon_to_mont(m, c);
-            store_vec(p + k, m);
+            ok &= fq_canon_to_mont(m[k], c);
+            store_vec(p + k, m[k]);
         }
-        if (!ok) atomicOr(err, 1);
+        if (!ok) {
+            atomicOr(err, 1);
+            continue;
+        }
+        // on the curve: y^2 = x^3 + b, b = 4 (G1) or 4 (1 + u) (G2); ark's CanonicalDeserialize of the
+        // PublicParameter rejects such points too (the subgroup check is not repeated: the PP is trusted
+        // input from setup, as in the reference's cache, commitment/mod.rs:41-62)
+        if constexpr (NF == 2) {
+            Fq y2, x3, b;
+            fe_sqr(y2, m[1]);
+            fe_sqr(x3, m[0]);
+            fe_mul(x3, x3, m[0]);
+            fe_one(b);
+            fe_add(b, b, b);
+            fe_add(b, b, b);
+            fe_add(x3, x3, b);
+            if (!fe_eq(y2, x3)) atomicOr(err, 2);
+        } else {
+            Fq2 x, y, y2, x3, b;
+            x.c0 = m[0], x.c1 = m[1], y.c0 = m[2], y.c1 = m[3];
+            f2_sqr(y2, y);
+            f2_sqr(x3, x);
+            f2_mul(x3, x3, x);
+            fe_one(b.c0);
+            fe_add(b.c0, b.c0, b.c0);
+            fe_add(b.c0, b.c0, b.c0);
+            b.c1 = b.c0;
+            f2_add(x3, x3, b);
+            if (!f2_eq(y2, x3)) atomicOr(err, 2);
+        }
     }
 }
 template <int NF>

@@ -164,7 +164,8 @@ std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len) {
     int herr = 0;
     SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
     C.sync();
-    if (herr) throw SpxError(kSerialization, "non-canonical coordinate in public parameters");
+    if (herr & 1) throw SpxError(kSerialization, "non-canonical coordinate in public parameters");
+    if (herr & 2) throw SpxError(kSerialization, "public parameter point not on the curve");
     pp_preprocess(C, *P);
     return P;
 }
@@ -1567,7 +1568,8 @@ std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t*
     SPX_HIP(hipMemcpyAsync(h.data(), out.p, out.bytes, hipMemcpyDeviceToHost, C.stream));
     SPX_HIP(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, C.stream));
     C.sync();
-    if (herr) throw SpxError(kSerialization, "non-canonical input");
+    if (herr & 1) throw SpxError(kSerialization, "non-canonical input");
+    if (herr & 2) throw SpxError(kSerialization, "base point not on the curve");
     std::vector<uint8_t> res(ps);
     if (g2)
         host::g2_to_uncompressed(res.data(), xyzz_bytes_to_affine<HFq2>(h.data()));

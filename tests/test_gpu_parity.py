@@ -70,6 +70,17 @@ def test_keygen_matches_oracle(spx, ctx, oc, nv):
     assert pp.serialize_uncompressed() == oc.PP.keygen(nv, 4242).serialize()
 
 
+@pytest.mark.parametrize("which", ["g1", "g2"])
+def test_pp_load_rejects_off_curve_point(spx, ctx, oc, which):
+    """a PP whose point is not on the curve is refused (SerializationError), as ark's deserialization does"""
+    nv = 4
+    b = bytearray(oc.PP.keygen(nv, 9).serialize())
+    off = 24 + 96 * 3 + 5 if which == "g1" else 16 + sum(8 + 96 * (16 >> i) for i in range(nv)) + 16 + 192 * 2 + 7
+    b[off] ^= 0x01  # a canonical coordinate that no longer satisfies y^2 = x^3 + b
+    with pytest.raises(spx.SerializationError):
+        spx.PublicParameter.load(ctx, bytes(b))
+
+
 def test_pp_load_roundtrip(spx, ctx, oc):
     b = oc.PP.keygen(5, 9).serialize()
     assert spx.PublicParameter.load(ctx, b).serialize_uncompressed() == b
@@ -143,7 +154,7 @@ def test_commit_open(spx, ctx, oc, nv):
     assert spx.MLPolyCommit.open(pp, table, point) == oc.open_(ppc, table, nv, point)
 
 
-CASES = [(0, 2, 1), (0, 4, 2), (0, 6, 3), (1, 7, 2), (2, 6, 2), (0, 10, 5), (1, 11, 5), (0, 12, 5)]
+CASES = [(0, 2, 1), (0, 4, 2), (0, 6, 3), (1, 7, 2), (2, 6, 2), (0, 10, 5), (1, 11, 5), (0, 12, 5), (3, 9, 3), (3, 12, 5)]
 
 
 @pytest.mark.parametrize("kind,log_n,log_v", CASES)

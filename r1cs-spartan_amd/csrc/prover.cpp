@@ -415,29 +415,31 @@ static void build_csc(const HostCsr& M, uint64_t n, std::vector<uint64_t>& cp, s
 }
 
 static void feed_matrix(Blake2s& h, const HostCsr& m) {
-    // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize }
-    std::vector<uint8_t> buf;
-    buf.reserve(1 << 16);
-    auto flush = [&]() {
-        h.update(buf.data(), buf.size());
-        buf.clear();
-    };
+    // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize },
+    // streamed through a 64 KiB staging block (u64 lengths, then (32-byte Fr, u64 column) per entry)
+    constexpr size_t kBlk = 1 << 16;
+    alignas(64) uint8_t buf[kBlk];
+    size_t len = 0;
     auto put64 = [&](uint64_t v) {
-        uint8_t b[8];
-        memcpy(b, &v, 8);
-        buf.insert(buf.end(), b, b + 8);
+        if (len + 8 > kBlk) h.update(buf, len), len = 0;
+        memcpy(buf + len, &v, 8);
+        len += 8;
     };
     put64(m.n);
+    const uint8_t* val = m.val.data();
+    const uint32_t* col = m.col.data();
     for (uint64_t x = 0; x < m.n; ++x) {
         put64(m.rp[x + 1] - m.rp[x]);
         for (uint64_t k = m.rp[x]; k < m.rp[x + 1]; ++k) {
-            buf.insert(buf.end(), m.val.data() + 32 * k, m.val.data() + 32 * k + 32);
-            put64(m.col[k]);
+            if (len + 40 > kBlk) h.update(buf, len), len = 0;
+            memcpy(buf + len, val + 32 * k, 32);
+            const uint64_t c = col[k];
+            memcpy(buf + len + 32, &c, 8);
+            len += 40;
         }
-        if (buf.size() > (1 << 16) - 4096) flush();
     }
     put64(m.n);
-    flush();
+    h.update(buf, len);
 }
 
 Blake2s absorb_matrices(const Index& I) {

@@ -1,0 +1,22 @@
+"""The product's host Blake2s (r1cs-spartan_amd/csrc/transcript.hpp, the Fiat-Shamir transcript's
+hash): RFC 7693 known answer and piecewise-update consistency, compiled from the header on the host
+(no GPU). Its use inside the transcript is pinned by every FS proof of the GPU parity tests."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_blake2s_kat_and_pieces(tmp_path):
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if not cxx:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path / "b2check")
+    subprocess.check_call([cxx, "-O2", "-std=c++17", "-w", "-I", os.path.join(ROOT, "r1cs-spartan_amd", "csrc"),
+                           "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
+                           os.path.join(ROOT, "tests", "native", "blake2s_check.cpp"), "-o", exe])
+    out = subprocess.check_output([exe], timeout=120).decode()
+    assert out.startswith("ok"), out

@@ -183,8 +183,8 @@ def issue_costs():
         return None
     out = {}
     for line in txt.splitlines():
-        if "cycles per wave-instruction" in line:
-            name = line.split("waves/SIMD")[0].strip()
+        if "cycles per wave-instruction" in line and "x 8 chains" in line:  # 8 independent chains per lane
+            name = line.split()[0]
             w = int(line.split("waves/SIMD")[1].split(":")[0])
             cyc = float(line.split("ms,")[1].split("cycles")[0])
             out["%s@%d" % (name, w)] = cyc
@@ -234,11 +234,16 @@ def roofline_valu(stats, dom):
     }
     ic = issue_costs()
     if ic and insts:
-        # instruction-mix ceiling: v_mad_u64_u32 is ~3/4 of the kernel's VALU instructions
-        c1 = ic.get("v_mad_u64_u32@1")
+        # instruction-mix ceiling (two waves per SIMD): ~70% of a mixed addition's VALU instructions are
+        # v_mad_u64_u32 (8 Fq2 products x 588 + 2 squares x 392 per lane), issue cost
+        # ic[mad@2]; the rest are single-issue ALU ops (ic[v_add_u32@2])
         roof["issue_costs_cycles"] = ic
-        if c1:
-            roof["frac_vs_mad_u64_rate_one_wave"] = round(insts * c1 / (1024 * 2.4e9) / avg_s, 4)
+        cm, ca = ic.get("v_mad_u64_u32@2"), ic.get("v_add_u32@2")
+        if cm and ca:
+            mix = 0.7 * cm + 0.3 * ca
+            roof["mix_ceiling_cycles_per_instr"] = round(mix, 2)
+            roof["achieved_cycles_per_instr"] = round(avg_s * 1024 * 2.4e9 / insts, 2)
+            roof["frac_vs_mix_ceiling"] = round(insts * mix / (1024 * 2.4e9) / avg_s, 4)
     roof["hbm"] = {
         "algorithmic_bytes_per_launch": per_launch,
         "achieved_GBs": round(per_launch / avg_s / 1e9, 1),

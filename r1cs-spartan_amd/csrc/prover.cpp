@@ -884,8 +884,13 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     }
     // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
     if (!o.stub) commit_launch(C, *P, z, n, G, rank);
+    // The shared level-0 opening proof is launched here, before any challenge, when the host has the
+    // matrix absorption to do meanwhile. With the index-cached transcript there is nothing to hide it
+    // behind: it then runs inside the first opening's batch (one MSM pipeline less on the critical
+    // path) and is reused by the second opening.
     const bool share0 = !o.stub && lvl0_local(L, G);
-    if (share0) lvl0_launch(C, *P, zl, L, G, rank);
+    const bool early0 = share0 && !(o.cached && I.has_cache);
+    if (early0) lvl0_launch(C, *P, zl, L, G, rank);
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
@@ -915,7 +920,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     mark("transcript_matrices", tp);
     Affine<HFq> com = o.stub ? Affine<HFq>{HFq::zero(), HFq::zero(), true} : commit_finish(C, G);
     Affine<HFq2> proof0{};
-    if (share0) proof0 = lvl0_finish(C, G);
+    if (early0) proof0 = lvl0_finish(C, G);
     Ser proof;
     {
         size_t m0 = proof.b.size();
@@ -930,7 +935,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, zl, L, pt1, G, rank, share0 ? &proof0 : nullptr);
+        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, zl, L, pt1, G, rank, early0 ? &proof0 : nullptr);
+        if (share0 && !early0) proof0 = op.proofs[0];
         size_t m0 = proof.b.size();
         ser_open(proof, op.eval, h_of(P), op.proofs);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);

@@ -55,7 +55,14 @@ static inline bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 
 // ====================================================================== public parameters
 int window_bits_for(uint64_t size) {
+    // SPX_WINDOW_BITS_LARGE (tuning): window bits for MSMs of >= 2^18 points (default 16)
+    static const int large = [] {
+        const char* e = getenv("SPX_WINDOW_BITS_LARGE");
+        const int v = e ? atoi(e) : 16;
+        return (v >= 12 && v <= 22) ? v : 16;
+    }();
     int k = size ? ilog2(size) : 0;
+    if (k >= 18) return large;
     if (k >= 14) return 16;
     return std::max(3, k - 2);
 }

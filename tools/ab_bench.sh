@@ -1,16 +1,23 @@
-# A/B of library builds on one box (run via gpurun from the repo root):
-#   tools/ab_bench.sh TAG ALT1.so [ALT2.so ...]
-# Rounds alternate the default build and every alternative (SPX_LIB_PATH), twice, with a short
-# bench (no CPU baseline, no C2 line); one JSON line per run into gpurun_out/<TAG>.jsonl.
+# A/B of library builds / environment settings on one box (run via gpurun from the repo root):
+#   tools/ab_bench.sh TAG ALT1 [ALT2 ...]
+# Each ALT is an alternative .so (used through SPX_LIB_PATH) or VAR=value settings joined by ','
+# (e.g. SPX_WINDOW_BITS_LARGE=18). Rounds alternate the default and every alternative, twice, with a
+# short bench (no CPU baseline, no C2 line); one JSON line per run into gpurun_out/<TAG>.jsonl.
 set -e
 TAG="$1"; shift
 OUT="gpurun_out/$TAG.jsonl"
 : > "$OUT"
+run() {  # $1 = label; remaining environment already exported by the caller
+  timeout -k 10 240 python bench.py --no-cpu --no-c2 --steps 3 --warmup 1 \
+    | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(json.dumps({'build': '$1', 'value': d['value'], 'ms_single_cached': d['ms_per_proof_single_cached_transcript'], 'kernels': d['kernels_ms_per_proof']}))" >> "$OUT"
+}
 for i in 1 2; do
-  timeout -k 10 200 python bench.py --no-cpu --no-c2 --steps 3 --warmup 1 \
-    | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(json.dumps({'build': 'default', 'round': $i, 'value': d['value'], 'ms_single_cached': d['ms_per_proof_single_cached_transcript'], 'kernels': d['kernels_ms_per_proof']}))" >> "$OUT"
+  run default
   for alt in "$@"; do
-    SPX_LIB_PATH="$alt" timeout -k 10 200 python bench.py --no-cpu --no-c2 --steps 3 --warmup 1 \
-      | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(json.dumps({'build': '$alt', 'round': $i, 'value': d['value'], 'ms_single_cached': d['ms_per_proof_single_cached_transcript'], 'kernels': d['kernels_ms_per_proof']}))" >> "$OUT"
+    if [[ "$alt" == *=* ]]; then
+      ( IFS=','; for kv in $alt; do export "$kv"; done; run "$alt" )
+    else
+      ( export SPX_LIB_PATH="$alt"; run "$alt" )
+    fi
   done
 done

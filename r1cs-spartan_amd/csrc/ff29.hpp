@@ -80,12 +80,19 @@ DEV void f29_one(F29& r) { f29_set(r, Q29::ONE); }
 #define SPX_F29_CHAINS 1
 #endif
 
+// An empty asm on each chain's sum before the join: integer addition is associative, and without
+// the barrier LLVM's reassociation folds the NC chains back into one serial v_mad_u64_u32 chain
+// (the generated code is then identical to NC = 1).
+DEV uint64_t f29_opaque(uint64_t x) {
+    asm("" : "+v"(x));
+    return x;
+}
 template <int NC>
 DEV uint64_t f29_join(const uint64_t (&ch)[NC], uint64_t carry) {
     if constexpr (NC == 1) return ch[0] + carry;
-    else if constexpr (NC == 2) return (ch[0] + ch[1]) + carry;
-    else if constexpr (NC == 3) return (ch[0] + ch[1]) + (ch[2] + carry);
-    else return ((ch[0] + ch[1]) + (ch[2] + ch[3])) + carry;
+    else if constexpr (NC == 2) return (f29_opaque(ch[0]) + f29_opaque(ch[1])) + carry;
+    else if constexpr (NC == 3) return (f29_opaque(ch[0]) + f29_opaque(ch[1])) + (f29_opaque(ch[2]) + carry);
+    else return ((f29_opaque(ch[0]) + f29_opaque(ch[1])) + (f29_opaque(ch[2]) + f29_opaque(ch[3]))) + carry;
 }
 
 // REDC(sum of NP products a_j b_j): NP = 1 (f29_mul) or 2 (f29_mul2, lazy reduction)

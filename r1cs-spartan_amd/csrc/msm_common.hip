@@ -173,6 +173,30 @@ uint32_t seg1_len(bool g2) {
     return g2 ? v2 : v1;
 }
 
+// The accumulation kernel's threads all run the same number of additions, so its duration is
+// (rounds of resident waves) x (one wave's chain of seg1 additions). A grid of 4.02 rounds takes as
+// long as 5: seg1 is lowered to the smallest value that keeps the round count, so the last round is
+// full. SPX_SEG1_FIT=0 keeps the fixed length (tuning).
+uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem) {
+    static const int on = [] {
+        const char* e = getenv("SPX_SEG1_FIT");
+        return e ? atoi(e) : 1;
+    }();
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 0;
+        return n;
+    }();
+    if (!on || cus <= 0 || refs == 0) return seg1;
+    const uint64_t slots = (uint64_t)cus * 4 * waves_per_simd * 64 / lanes_per_elem;  // resident elements
+    const uint64_t nthr = (refs + seg1 - 1) / seg1;
+    const uint64_t rounds = (nthr + slots - 1) / slots;
+    if (rounds > 16) return seg1;
+    const uint64_t fit = (refs + rounds * slots - 1) / (rounds * slots);
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(seg1, fit));
+}
+
 MsmWorkspace* msm_ws_create() { return new MsmWorkspace(); }
 void msm_ws_destroy(MsmWorkspace* ws) { delete ws; }
 

@@ -308,7 +308,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     const uint64_t tot_refs = so.tot_refs;
     // level 1: affine references -> XYZZ partials, one per segment of kSeg references
     const size_t psz = sizeof(Xyzz<F>);
-    const uint32_t kSeg1 = seg1_len(g2);
+    const uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));

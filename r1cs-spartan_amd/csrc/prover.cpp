@@ -61,9 +61,15 @@ int window_bits_for(uint64_t size) {
         const int v = e ? atoi(e) : 16;
         return (v >= 12 && v <= 22) ? v : 16;
     }();
+    // SPX_WINDOW_MID (tuning): for 2^14..2^17 points, c = min(16, log2(size) - MID) (0: 16)
+    static const int mid = [] {
+        const char* e = getenv("SPX_WINDOW_MID");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 0 && v <= 6) ? v : 0;
+    }();
     int k = size ? ilog2(size) : 0;
     if (k >= 18) return large;
-    if (k >= 14) return 16;
+    if (k >= 14) return mid ? std::min(16, k - mid) : 16;
     return std::max(3, k - 2);
 }
 static int windows_for(int c) { return (256 + c - 1) / c; }

@@ -45,6 +45,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 2.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_kernels.json")
 ISSUE_FILE = os.path.join(ROOT, "profiles", "r02_ubench_issue.txt")
+MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
 KSYM = {"sc1_round": "k_sc1_round<true>", "sc2_round": "k_sc2_round<true>", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
@@ -254,8 +255,27 @@ def roofline_valu(stats, dom):
         "traffic_source": "profiles/pmc_kernels.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
     }
     if d.get("ops"):
-        roof["mixed_additions_per_s_live"] = round(d["ops"] / d["launches"] / avg_s, 1)
+        live = d["ops"] / d["launches"] / avg_s
+        roof["mixed_additions_per_s_live"] = round(live, 1)
+        rr = madd_register_resident()
+        if rr and dom == "msm_acc_g2":
+            # the same formula with every operand in registers (no loads, no bucket logic, full grid):
+            # what the accumulation kernel would reach if its memory side and its grid tail were free
+            roof["register_resident_madd_per_s"] = rr
+            roof["frac_vs_register_resident_madd"] = round(live / rr, 4)
+            roof["register_resident_source"] = os.path.relpath(MADD_FILE, ROOT) + " (tools/ubench_madd.hip, 2 waves/SIMD)"
     return roof
+
+
+def madd_register_resident():
+    """lane-pair G2 mixed additions per second of x29_madd on register-resident operands"""
+    try:
+        for line in open(MADD_FILE):
+            if line.startswith("chains 1 madd") and "waves/SIMD 2" in line:
+                return float(line.split(",")[-1].split("G iterations/s")[0]) * 1e9
+    except OSError:
+        pass
+    return None
 
 
 def roofline_hbm(stats):

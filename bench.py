@@ -317,6 +317,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--no-cached", action="store_true",
+                    help="skip the index-cached transcript runs (profiling: one launch mix in the whole process)")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 (sumcheck-only) line of the default run")
     ap.add_argument("--shard", default="proof", choices=["batch", "proof"],
                     help="N > 1 headline: 'proof' = every proof split over all ranks (strong, per-round exchange); "
@@ -448,22 +450,28 @@ def main():
         stats = kernel_stats(spx, L, hctx, args.steps * (P // B))  # ctx 0 proves P / B proofs per step
         spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
     ref = check_batch(proofs)
-    # ---- single-proof latency (one proof at a time), with and without the index-cached transcript
+    # ---- single-proof latency (one proof at a time), with and without the index-cached transcript.
+    # Kernel durations with one proof at a time (no other proof sharing the GPU) come from the
+    # per-proof-absorbed loop: the same launch mix as the batched proofs (level 0 as its own MSM)
+    if not args.no_stats:
+        spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
     p1, elapsed_single = timed(single_fn(hctx, hpk))
     assert p1 == ref[0], "single proof differs from the batched one"
     phases = hctx.last_timings()
-    if not args.no_stats:  # kernel durations with one proof at a time (no other proof sharing the GPU)
-        spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
-    p1c, elapsed_single_c = timed(single_fn(hctx, hpk, cached=True))
-    assert p1c == ref[0], "cached-transcript single proof differs"
-    phases_c = hctx.last_timings()
     alone = {}
     if not args.no_stats:
         alone = kernel_stats(spx, L, hctx, args.steps)
         spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
+    elapsed_single_c = elapsed_cached = None
+    phases_c = {}
+    if not args.no_cached:
+        p1c, elapsed_single_c = timed(single_fn(hctx, hpk, cached=True))
+        assert p1c == ref[0], "cached-transcript single proof differs"
+        phases_c = hctx.last_timings()
     # ---- index-cached transcript throughput (matrix absorption moved to index time; bit-identical)
-    p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True))
-    check_batch(p2, ref)
+    if not args.no_cached:
+        p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True))
+        check_batch(p2, ref)
     # ---- N > 1: the other shard mode (throughput, and the proof-sharded single-proof latency)
     other = None
     if world > 1 and not args.no_other:
@@ -478,9 +486,9 @@ def main():
         other = [el, el1]
 
     ms = elapsed / args.steps * 1e3  # per step (P proofs)
-    ms_c = elapsed_cached / args.steps * 1e3
+    ms_c = elapsed_cached / args.steps * 1e3 if elapsed_cached else 0.0
     ms_1 = elapsed_single / args.steps * 1e3
-    ms_1c = elapsed_single_c / args.steps * 1e3
+    ms_1c = elapsed_single_c / args.steps * 1e3 if elapsed_single_c else 0.0
     ms_o = ms_o1 = None
     if dist is not None:
         import torch
@@ -554,10 +562,10 @@ def main():
         },
         "ms_per_proof_single": round(ms_1, 3),
         "value_single_proof": round(n / (ms_1 / 1e3), 1),
-        "ms_per_proof_single_cached_transcript": round(ms_1c, 3),
-        "value_single_proof_cached_transcript": round(n / (ms_1c / 1e3), 1),
-        "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1),
-        "ms_per_step_index_cached_transcript": round(ms_c, 3),
+        "ms_per_proof_single_cached_transcript": round(ms_1c, 3) if ms_1c else None,
+        "value_single_proof_cached_transcript": round(n / (ms_1c / 1e3), 1) if ms_1c else None,
+        "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1) if ms_c else None,
+        "ms_per_step_index_cached_transcript": round(ms_c, 3) if ms_c else None,
         "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
         "phases_ms_cached_transcript": {k: round(v / 1e3, 3) for k, v in phases_c.items()},
         "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in alone.items()},

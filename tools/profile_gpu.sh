@@ -19,7 +19,9 @@ export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES="${PROF_HW_QUEUES:-16}"
 [ -x "$ROOT/tools/calib_stream" ] || hipcc -O2 --offload-arch=gfx950 "$ROOT/tools/calib_stream.hip" -o "$ROOT/tools/calib_stream"
 cd /tmp
-B1="--steps 1 --warmup 1 --no-cpu --no-c2 --inflight 1 --proofs-per-step 4"
+# one proof in flight, no index-cached runs: every G2 launch of the process is one of the three per
+# proof that bench.py's "alone" statistics time (level 0, the two opening batches)
+B1="--steps 1 --warmup 1 --no-cpu --no-c2 --no-cached --inflight 1 --proofs-per-step 4"
 if [ -z "$PROF_SKIP_TRACE" ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$RAW/trace" -o run --output-format csv -- \
     python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --no-c2 > "$OUT/bench_traced.json" 2> "$OUT/trace.err"

@@ -45,22 +45,58 @@ DEV F29 f29_select(bool c, const F29& a, const F29& b) {
     return r;
 }
 
-template <>
-struct Ops29<FP29> {
-    // operands up to 8p per coefficient (the partner's b enters as 8p - b')
-    static DEV void mul(FP29& r, const FP29& a, const FP29& b) {
+// b0 (the even lane's value) on both lanes of the pair: quad_perm [0,0,2,2]
+DEV uint32_t pair_even(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xF, 0xF, false); }
+// b1 (the odd lane's value) on both lanes: quad_perm [1,1,3,3]
+DEV uint32_t pair_odd_val(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xF5, 0xF, 0xF, false); }
+
+// 16p with every limb but the top raised by 2^29 (borrowed from the next limb): k_i - z_i is then
+// non-negative and < 2^30 for every normalized z < 8p, so 16p - z needs no borrow chain
+DEV constexpr uint32_t k16(int i) {
+    return i == 0 ? Q29::P16[0] + (1u << 29) : i < 13 ? Q29::P16[i] + (1u << 29) - 1u : Q29::P16[13] - 1u;
+}
+
+// Two forms of the lane pair, identical in value and layout, differing only in how a product
+// prepares the partner's operand:
+//   FP29  (weighting and partial levels): y2 = 8p - b' by a borrow-chain subtraction;
+//   FP29A (the bucket accumulation, k_accum_aff): y1 and b1 come straight from DPP quad-permutes and
+//         y2 = 16p - b1 from the borrow-free k16 form (non-normalized limbs < 2^30). Columns stay below
+//         2^64: 14 products < 2^58 (a y1) + 14 < 2^59 (a' y2) + 14 m p < 2^58 = 56 x 2^58; the REDC
+//         input a0 b0 + a1 (16p - b1) < 192 p^2 < 2^406 p, so the result is < 2p as before.
+// FP29A is 3% faster in the accumulation (profiles/r02_ab9_xad.jsonl); in the weighting kernels,
+// which already spill at 256 registers, it spills more and is slower, so they keep FP29.
+struct FP29A {
+    F29 v;
+};
+
+template <class P, bool kBorrowFree>
+struct PairOps {
+    static DEV void mul(P& r, const P& a, const P& b) {
         const bool odd = pair_odd();
-        const F29 ap = pair_swap(a.v), bp = pair_swap(b.v);
-        F29 z, nbp;
-        f29_zero(z);
-        f29_sub<8>(nbp, z, bp);
-        const F29 y1 = f29_select(odd, bp, b.v);
-        const F29 y2 = f29_select(odd, b.v, nbp);
-        f29_mul2(r.v, a.v, y1, ap, y2);
+        if constexpr (kBorrowFree) {
+            const uint32_t msk = odd ? 0u : 0xffffffffu;
+            F29 ap, y1, y2;
+#pragma unroll
+            for (int i = 0; i < 14; ++i) {
+                ap.v[i] = pair_swap(a.v.v[i]);
+                y1.v[i] = pair_even(b.v.v[i]);
+                const uint32_t z = pair_odd_val(b.v.v[i]);
+                y2.v[i] = (z ^ msk) + (msk & (k16(i) + 1u));  // even: k_i - z_i; odd: z_i
+            }
+            f29_mul2(r.v, a.v, y1, ap, y2);
+        } else {
+            const F29 ap = pair_swap(a.v), bp = pair_swap(b.v);
+            F29 z, nbp;
+            f29_zero(z);
+            f29_sub<8>(nbp, z, bp);
+            const F29 y1 = f29_select(odd, bp, b.v);
+            const F29 y2 = f29_select(odd, b.v, nbp);
+            f29_mul2(r.v, a.v, y1, ap, y2);
+        }
     }
     // (a0 + a1)(a0 - a1 + KB p) on the even lane, (a0 + a0) a1 on the odd one; KB bounds c1
     template <int KB>
-    static DEV void sqr_b(FP29& r, const FP29& a) {
+    static DEV void sqr_b(P& r, const P& a) {
         const bool odd = pair_odd();
         const F29 ap = pair_swap(a.v);
         F29 s, d, x, y;
@@ -71,41 +107,50 @@ struct Ops29<FP29> {
         x = f29_select(odd, x, s);
         f29_mul(r.v, x, y);
     }
-    static DEV void sqr(FP29& r, const FP29& a) { sqr_b<8>(r, a); }
-    static DEV void add(FP29& r, const FP29& a, const FP29& b) { f29_add(r.v, a.v, b.v); }
+    static DEV void sqr(P& r, const P& a) { sqr_b<8>(r, a); }
+    static DEV void add(P& r, const P& a, const P& b) { f29_add(r.v, a.v, b.v); }
     template <int K>
-    static DEV void sub(FP29& r, const FP29& a, const FP29& b) {
+    static DEV void sub(P& r, const P& a, const P& b) {
         f29_sub<K>(r.v, a.v, b.v);
     }
     template <int K>
-    static DEV void reduce(FP29& x) {
+    static DEV void reduce(P& x) {
         f29_reduce<K>(x.v);
     }
-    static DEV bool zero2(const FP29& x) { return pair_all(f29_zero2(x.v)); }
-    static DEV bool zero4(const FP29& x) { return pair_all(f29_zero4(x.v)); }
+    static DEV bool zero2(const P& x) { return pair_all(f29_zero2(x.v)); }
+    static DEV bool zero4(const P& x) { return pair_all(f29_zero4(x.v)); }
     template <int K>
-    static DEV bool zero_lt(const FP29& x) {
+    static DEV bool zero_lt(const P& x) {
         return pair_all(f29_zero_lt<K>(x.v));
     }
-    static DEV bool is_zero_raw(const FP29& x) { return pair_all(f29_is_zero_raw(x.v)); }
-    static DEV void zero(FP29& r) { f29_zero(r.v); }
-    static DEV void one(FP29& r) {
+    static DEV bool is_zero_raw(const P& x) { return pair_all(f29_is_zero_raw(x.v)); }
+    static DEV void zero(P& r) { f29_zero(r.v); }
+    static DEV void one(P& r) {
         if (pair_odd())
             f29_zero(r.v);
         else
             f29_one(r.v);
     }
 };
+template <>
+struct Ops29<FP29> : PairOps<FP29, false> {};
+template <>
+struct Ops29<FP29A> : PairOps<FP29A, true> {};
 
 // ---- storage: the lane's half of a packed (12 x 32-bit words per Fq) Fq2 coordinate
-DEV void fp29_unpack(FP29& r, const Fq2& s) { f29_unpack(r.v, pair_odd() ? s.c1.v : s.c0.v); }
+template <class P>
+DEV void fp29_unpack(P& r, const Fq2& s) {
+    f29_unpack(r.v, pair_odd() ? s.c1.v : s.c0.v);
+}
 // ld / st of one lane's coefficient of coordinate k of a point at p (Fq2 coordinates, c0 then c1)
-DEV void fp29_ld(FP29& r, const Fq2* coord) {
+template <class P>
+DEV void fp29_ld(P& r, const Fq2* coord) {
     Fq w;
     load_vec(w, pair_odd() ? &coord->c1 : &coord->c0);
     f29_unpack(r.v, w.v);
 }
-DEV void fp29_st(Fq2* coord, const FP29& r) {
+template <class P>
+DEV void fp29_st(Fq2* coord, const P& r) {
     Fq w;
     f29_pack(w.v, r.v);
     store_vec(pair_odd() ? &coord->c1 : &coord->c0, w);

@@ -28,6 +28,7 @@ struct AffRaw {
 template <>
 struct Acc<Fq> {
     using T = F29;
+    using TA = F29;  // the accumulation kernel's element type
     static constexpr int kLanes = 1, kWaves = SPX_G1_WAVES;
     static DEV void ld_raw(AffRaw& a, const Aff<Fq>* p) { load_vec(*(Aff<Fq>*)&a, p); }
     static DEV void unpack(T& x, T& y, const AffRaw& a) {
@@ -46,21 +47,25 @@ struct Acc<Fq> {
 template <>
 struct Acc<Fq2> {
     using T = FP29;
+    using TA = FP29A;  // borrow-free operand preparation in the accumulation only (fq2pair.hpp)
     static constexpr int kLanes = 2, kWaves = SPX_G2_WAVES;
     static DEV void ld_raw(AffRaw& a, const Aff<Fq2>* p) {
         const bool odd = pair_odd();
         load_vec(a.x, odd ? &p->x.c1 : &p->x.c0);
         load_vec(a.y, odd ? &p->y.c1 : &p->y.c0);
     }
-    static DEV void unpack(T& x, T& y, const AffRaw& a) {
+    template <class P>
+    static DEV void unpack(P& x, P& y, const AffRaw& a) {
         f29_unpack(x.v, a.x.v);
         f29_unpack(y.v, a.y.v);
     }
-    static DEV void ld_aff(T& x, T& y, const Aff<Fq2>* p) {
+    template <class P>
+    static DEV void ld_aff(P& x, P& y, const Aff<Fq2>* p) {
         fp29_ld(x, &p->x);
         fp29_ld(y, &p->y);
     }
-    static DEV bool aff_sentinel(const T& x, const T& y) {
+    template <class P>
+    static DEV bool aff_sentinel(const P& x, const P& y) {
         return pair_all(f29_is_zero_raw(x.v) && f29_is_zero_raw(y.v));
     }
     static DEV void ld(X29<T>& r, const Xyzz<Fq2>* p) {
@@ -69,7 +74,8 @@ struct Acc<Fq2> {
         fp29_ld(r.zz, &p->zz);
         fp29_ld(r.zzz, &p->zzz);
     }
-    static DEV void st(Xyzz<Fq2>* p, const X29<T>& r) {
+    template <class P>
+    static DEV void st(Xyzz<Fq2>* p, const X29<P>& r) {
         fp29_st(&p->x, r.x);
         fp29_st(&p->y, r.y);
         fp29_st(&p->zz, r.zz);
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
                                                                       const Aff<F>* __restrict__ pts,
                                                                       Xyzz<F>* __restrict__ out, uint32_t seg1) {
     using A = Acc<F>;
-    using T = typename A::T;
+    using T = typename A::TA;
     const uint32_t t = (uint32_t)acc_elem<F>();
     const uint32_t total = off[nb];
     uint32_t e = t * seg1;

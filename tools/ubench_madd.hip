@@ -2,7 +2,7 @@
 //   k_madd: x29_madd (madd-2008-s, lane-pair Fq2) in a loop — the hot loop of k_accum_aff<Fq2>,
 //           ~100 KB of straight-line code per iteration;
 //   k_mul : the lane-pair Fq2 product alone, 10 per iteration in a non-unrolled loop (~5 KB of code).
-// Built once per SPX_F29_CHAINS value (tools/ubench_madd.sh). The per-product cost of k_madd over
+// Built once per SPX_F29_CHAINS value (-DSPX_F29_CHAINS=N). The per-product cost of k_madd over
 // that of k_mul separates the formula's own overhead (additions, selects, instruction supply) from
 // the product's issue cost. Operands are random field-sized values, not curve points: the formula's
 // cost does not depend on them (no exceptional branch is taken).
@@ -36,8 +36,8 @@ DEV void rnd(F29& f, uint32_t& s) {
 template <int W>
 __global__ __launch_bounds__(64, W) void k_madd(uint32_t* out, uint32_t seed, int iters) {
     uint32_t s = seed ^ ((blockIdx.x * 64 + threadIdx.x) >> 1) * 2654435761u;
-    X29<FP29> acc;
-    FP29 px, py;
+    X29<FP29A> acc;
+    FP29A px, py;
     rnd(acc.x.v, s);
     rnd(acc.y.v, s);
     rnd(acc.zz.v, s);
@@ -57,14 +57,14 @@ __global__ __launch_bounds__(64, W) void k_madd(uint32_t* out, uint32_t seed, in
 template <int W>
 __global__ __launch_bounds__(64, W) void k_mul(uint32_t* out, uint32_t seed, int iters) {
     uint32_t s = seed ^ ((blockIdx.x * 64 + threadIdx.x) >> 1) * 2654435761u;
-    FP29 a, b;
+    FP29A a, b;
     rnd(a.v, s);
     rnd(b.v, s);
     for (int i = 0; i < iters; ++i) {
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
-            FP29 r;
-            Ops29<FP29>::mul(r, a, b);
+            FP29A r;
+            Ops29<FP29A>::mul(r, a, b);
             a = b;
             b = r;
         }

@@ -99,6 +99,20 @@ struct PairOps {
     static DEV void sqr_b(P& r, const P& a) {
         const bool odd = pair_odd();
         const F29 ap = pair_swap(a.v);
+        if constexpr (kBorrowFree) {
+            // even: (a0 + a1) [limb sums, < 2^30, no carry] x (a0 - a1 + KB p) [normalized];
+            // odd: a0 [normalized] x (a1 + a1) [limb sums, < 2^30]. One factor of every limb product
+            // is < 2^29: columns <= 14 x 2^59 + 14 m p < 2^58 = 42 x 2^58. Same values as below.
+            F29 d, x, y;
+            f29_sub<KB>(d, a.v, ap);
+#pragma unroll
+            for (int i = 0; i < 14; ++i) {
+                x.v[i] = odd ? ap.v[i] : a.v.v[i] + ap.v[i];
+                y.v[i] = odd ? a.v.v[i] + a.v.v[i] : d.v[i];
+            }
+            f29_mul(r.v, x, y);
+            return;
+        }
         F29 s, d, x, y;
         f29_add(s, a.v, ap);          // even: a0 + a1
         f29_sub<KB>(d, a.v, ap);      // even: a0 - a1 + KB p

@@ -194,7 +194,9 @@ uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_pe
     const uint64_t rounds = (nthr + slots - 1) / slots;
     if (rounds > 16) return seg1;
     const uint64_t fit = (refs + rounds * slots - 1) / (rounds * slots);
-    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(seg1, fit));
+    // floor 8: below one round the grid cannot fill the GPU anyway, and every reference moved out of
+    // the mixed-addition chains costs a full XYZZ addition in the partial levels instead
+    return (uint32_t)std::min<uint64_t>(seg1, std::max<uint64_t>(fit, std::min<uint32_t>(seg1, 8)));
 }
 
 MsmWorkspace* msm_ws_create() { return new MsmWorkspace(); }

@@ -64,6 +64,30 @@ def test_msm_g2_degenerate_scalars(spx, ctx, oc, scalar):
     assert spx.msm_g2(ctx, g2[: 192 * n], s * n) == oc.msm_g2(g2[: 192 * n], s * n, n)
 
 
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_repeated_bases_doubling_and_cancellation(spx, ctx, oc, group):
+    """bases repeated inside one bucket: the accumulation meets P + P (its doubling branch) and
+    P + (-P) (scalars s and r - s give opposite digits: the infinity branch), on every window."""
+    g1, g2 = _pp_bases(oc, 4, 11)
+    w = 96 if group == "g1" else 192
+    src = g1 if group == "g1" else g2
+    pts = [src[w * i : w * (i + 1)] for i in range(3)]
+    s = (0x1234567890ABCDEF1234567 * 131).to_bytes(32, "little")
+    t = (R - int.from_bytes(s, "little")).to_bytes(32, "little")
+    u = (0xFEDCBA9876543210 << 64 | 77).to_bytes(32, "little")
+    bases, sc = [], []
+    for k, (pi, reps) in enumerate([(0, 8), (1, 5), (2, 3)]):
+        bases += [pts[pi]] * reps
+        sc += [s] * reps
+    bases += [pts[0], pts[1], pts[1], pts[2]]  # cancellations against the runs above, and a new scalar
+    sc += [t, t, u, u]
+    b, c, n = b"".join(bases), b"".join(sc), len(bases)
+    if group == "g1":
+        assert spx.msm_g1(ctx, b, c) == oc.msm_g1(b, c, n)
+    else:
+        assert spx.msm_g2(ctx, b, c) == oc.msm_g2(b, c, n)
+
+
 @pytest.mark.parametrize("nv", [3, 6])
 def test_keygen_matches_oracle(spx, ctx, oc, nv):
     pp = spx.MLProofForR1CS.setup(ctx, nv, 4242)

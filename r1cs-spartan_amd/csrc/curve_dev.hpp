@@ -19,6 +19,14 @@ struct Xyzz {
     F x, y, zz, zzz;
 };
 using G1Aff = Aff<Fq>;
+// A G1 point of the MSM window tables in a 128-byte slot: a 96-byte point at a 96-byte pitch
+// straddles two 128-byte lines for two points in three, so every random gather fetched ~2x its bytes
+// (profiles/r01_pmc_traffic.json); one slot per line fetches each point with one line.
+struct G1Slot {
+    G1Aff p;
+    uint32_t pad[8];
+};
+static_assert(sizeof(G1Slot) == 128, "G1 table slot");
 using G2Aff = Aff<Fq2>;
 using G1Xyzz = Xyzz<Fq>;
 using G2Xyzz = Xyzz<Fq2>;

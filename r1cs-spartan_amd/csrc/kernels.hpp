@@ -149,7 +149,7 @@ void msm_ws_destroy(MsmWorkspace* ws);
 
 // Runs a batch of MSMs on `s`; out_xyzz receives one XYZZ point per instance (G1: 4 x 48 B,
 // G2: 4 x 96 B, Montgomery limbs). Synchronises once on `s` to size the accumulation levels.
-void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G1Aff* pts, const Fr* scalars,
+void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G1Slot* pts, const Fr* scalars,
                 void* out_xyzz_dev, hipStream_t s);
 void msm_run_g2(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G2Aff* pts, const Fr* scalars,
                 void* out_xyzz_dev, hipStream_t s);

@@ -8,7 +8,7 @@
 
 namespace spx {
 
-void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts, int ninst, const G1Aff* pts, const Fr* scalars, void* out,
+void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts, int ninst, const G1Slot* pts, const Fr* scalars, void* out,
                 hipStream_t s) {
     msm_run_t<Fq>(ws, insts, ninst, pts, scalars, out, s);
 }

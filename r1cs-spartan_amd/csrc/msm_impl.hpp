@@ -27,15 +27,16 @@ struct AffRaw {
 };
 template <>
 struct Acc<Fq> {
+    using Pt = G1Slot;  // window-table element: one 128-byte line per point
     using T = F29;
     using TA = F29;  // the accumulation kernel's element type
     static constexpr int kLanes = 1, kWaves = SPX_G1_WAVES;
-    static DEV void ld_raw(AffRaw& a, const Aff<Fq>* p) { load_vec(*(Aff<Fq>*)&a, p); }
+    static DEV void ld_raw(AffRaw& a, const G1Slot* p) { load_vec(*(Aff<Fq>*)&a, &p->p); }
     static DEV void unpack(T& x, T& y, const AffRaw& a) {
         f29_unpack(x, a.x.v);
         f29_unpack(y, a.y.v);
     }
-    static DEV void ld_aff(T& x, T& y, const Aff<Fq>* p) {
+    static DEV void ld_aff(T& x, T& y, const G1Slot* p) {
         AffRaw a;
         ld_raw(a, p);
         unpack(x, y, a);
@@ -46,6 +47,7 @@ struct Acc<Fq> {
 };
 template <>
 struct Acc<Fq2> {
+    using Pt = Aff<Fq2>;  // 192 bytes: 1.5 lines, the lane pair's halves 96 bytes each
     using T = FP29;
     using TA = FP29A;  // borrow-free operand preparation in the accumulation only (fq2pair.hpp)
     static constexpr int kLanes = 2, kWaves = SPX_G2_WAVES;
@@ -103,7 +105,7 @@ template <class F>
 __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint32_t* __restrict__ off, uint32_t nb,
                                                                       const uint32_t* __restrict__ pfx,
                                                                       const uint32_t* __restrict__ refs,
-                                                                      const Aff<F>* __restrict__ pts,
+                                                                      const typename Acc<F>::Pt* __restrict__ pts,
                                                                       Xyzz<F>* __restrict__ out, uint32_t seg1) {
     using A = Acc<F>;
     using T = typename A::TA;
@@ -305,7 +307,7 @@ __global__ void k_tree_out(int ninst, const uint32_t* __restrict__ node_off, con
 }
 
 template <class F>
-static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<F>* pts, const Fr* scalars,
+static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const typename Acc<F>::Pt* pts, const Fr* scalars,
                       void* out_dev, hipStream_t s) {
     if (ninst <= 0) return;
     MsmSorted so = msm_sort(ws, ih, ninst, scalars, s);
@@ -324,7 +326,8 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Aff<
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, so.soa, so.refs, pts, PA,
                        kSeg1);
-    // algorithmic bytes: every reference (4 B) and its affine point once, one XYZZ partial per segment
+    // algorithmic bytes: every reference (4 B) and its affine point once (96 / 192 B, not the slot's
+    // padding), one XYZZ partial per segment
     kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s, (double)tot_refs);
     uint32_t* cur_cnt = so.segcnt;
     uint32_t* cur_off = so.soa;

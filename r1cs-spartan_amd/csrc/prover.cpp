@@ -74,8 +74,9 @@ int window_bits_for(uint64_t size) {
 }
 static int windows_for(int c) { return (256 + c - 1) / c; }
 
-template <class A>
-static void precompute_level(Ctx& C, const A* raw, uint64_t count, bool pair, int c, int W, A* dst) {
+// dst: G2Aff rows, or G1Slot rows (128-byte slots) for G1
+template <class A, class D>
+static void precompute_level(Ctx& C, const A* raw, uint64_t count, bool pair, int c, int W, D* dst) {
     // chunked to bound the XYZZ temporary: tmp XYZZ [W][chunk] -> affine [W][chunk] -> dst rows (pitch count)
     const uint64_t chunk = std::min<uint64_t>(count, 1ull << 18);
     const size_t xyzz_sz = 2 * sizeof(A);
@@ -87,8 +88,14 @@ static void precompute_level(Ctx& C, const A* raw, uint64_t count, bool pair, in
             precompute_windows_g1((const G1Aff*)src, cn, pair, c, W, aff.as<G1Aff>(), tmp.p, C.stream);
         else
             precompute_windows_g2((const G2Aff*)src, cn, pair, c, W, aff.as<G2Aff>(), tmp.p, C.stream);
-        SPX_HIP(hipMemcpy2DAsync(dst + j0, sizeof(A) * count, aff.p, sizeof(A) * cn, sizeof(A) * cn, W,
-                                 hipMemcpyDeviceToDevice, C.stream));
+        if constexpr (sizeof(D) == sizeof(A)) {
+            SPX_HIP(hipMemcpy2DAsync(dst + j0, sizeof(A) * count, aff.p, sizeof(A) * cn, sizeof(A) * cn, W,
+                                     hipMemcpyDeviceToDevice, C.stream));
+        } else {  // one point per slot: a 2-D copy per window, rows = points (pitch 96 -> 128 bytes)
+            for (int w = 0; w < W; ++w)
+                SPX_HIP(hipMemcpy2DAsync(dst + (uint64_t)w * count + j0, sizeof(D), aff.as<A>() + (uint64_t)w * cn,
+                                         sizeof(A), sizeof(A), cn, hipMemcpyDeviceToDevice, C.stream));
+        }
     }
     C.sync();
 }
@@ -98,8 +105,8 @@ void pp_preprocess(Ctx& C, PP& P) {
     const uint64_t n = 1ull << nv;
     P.g1_c = window_bits_for(n);
     P.g1_W = windows_for(P.g1_c);
-    P.g1_pre.alloc(sizeof(G1Aff) * n * P.g1_W);
-    precompute_level<G1Aff>(C, P.g1_level(0), n, false, P.g1_c, P.g1_W, P.g1_pre.as<G1Aff>());
+    P.g1_pre.alloc(sizeof(G1Slot) * n * P.g1_W);
+    precompute_level(C, P.g1_level(0), n, false, P.g1_c, P.g1_W, P.g1_pre.as<G1Slot>());
     P.g2_off.assign(nv + 1, 0);
     P.g2_c.assign(nv, 0);
     P.g2_W.assign(nv, 0);
@@ -115,7 +122,7 @@ void pp_preprocess(Ctx& C, PP& P) {
     P.g2_pre.alloc(sizeof(G2Aff) * std::max<uint64_t>(tot, 1));
     for (int i = 0; i < nv; ++i) {
         uint64_t cnt = 1ull << (nv - i - 1);
-        precompute_level<G2Aff>(C, P.g2_level(i), cnt, true, P.g2_c[i], P.g2_W[i], P.g2_pre.as<G2Aff>() + P.g2_off[i]);
+        precompute_level(C, P.g2_level(i), cnt, true, P.g2_c[i], P.g2_W[i], P.g2_pre.as<G2Aff>() + P.g2_off[i]);
     }
 }
 
@@ -615,7 +622,7 @@ static void commit_launch(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, in
     inst.c = (uint32_t)P.g1_c;
     inst.W = (uint32_t)P.g1_W;
     void* out = C.buf(Ctx::kSlotCommit, 4 * sizeof(Fq));
-    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Aff>(), z_full, out, C.stream);
+    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Slot>(), z_full, out, C.stream);
     SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, 4 * sizeof(Fq), 4 << 10), out, 4 * sizeof(Fq),
                            hipMemcpyDeviceToHost, C.stream));
 }
@@ -1575,15 +1582,15 @@ std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t*
     I.W = (uint32_t)windows_for((int)I.c);
     I.size = (uint32_t)n;
     I.stride = (uint32_t)n;
-    DevMem pre(ps * n * I.W), out(4 * (g2 ? sizeof(Fq2) : sizeof(Fq)));
+    DevMem pre((g2 ? sizeof(G2Aff) : sizeof(G1Slot)) * n * I.W), out(4 * (g2 ? sizeof(Fq2) : sizeof(Fq)));
     if (g2)
-        precompute_level<G2Aff>(C, raw.as<G2Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G2Aff>());
+        precompute_level(C, raw.as<G2Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G2Aff>());
     else
-        precompute_level<G1Aff>(C, raw.as<G1Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G1Aff>());
+        precompute_level(C, raw.as<G1Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G1Slot>());
     if (g2)
         msm_run_g2(C.msm, &I, 1, pre.as<G2Aff>(), sc.as<Fr>(), out.p, C.stream);
     else
-        msm_run_g1(C.msm, &I, 1, pre.as<G1Aff>(), sc.as<Fr>(), out.p, C.stream);
+        msm_run_g1(C.msm, &I, 1, pre.as<G1Slot>(), sc.as<Fr>(), out.p, C.stream);
     std::vector<uint8_t> h(out.bytes);
     int herr = 0;
     SPX_HIP(hipMemcpyAsync(h.data(), out.p, out.bytes, hipMemcpyDeviceToHost, C.stream));

@@ -173,9 +173,11 @@ DEV void x29_madd(X29<F>& p, const F& ax, const F& ay_in, bool neg) {
     O::add(t, Q, Q);                 // < 4p
     O::template sub<4>(w, w, t);     // X3 < 8p (loose)
     O::template sub<8>(t, Q, w);     // < 10p
-    O::mul(t, t, R);                 // (t, R): the second operand's c1 must stay < 8p
-    O::mul(S2, p.y, PPP);
-    O::template sub<2>(p.y, t, S2);  // Y3 < 4p (loose)
+    // Y3 = t R - Y1 PPP = t R + (4p - Y1) PPP in one reduction where the field form allows it
+    // (mul_sum: < 2p fused, < 4p otherwise); R's and PPP's c1 stay < 8p as the products require
+    O::zero(S2);
+    O::template sub<4>(S2, S2, p.y);  // 4p - Y1 (Y1 < 4p), < 4p
+    O::mul_sum(p.y, t, R, S2, PPP);   // Y3 < 4p (loose)
     p.x = w;
     O::mul(p.zz, p.zz, PP);
     O::mul(p.zzz, p.zzz, PPP);

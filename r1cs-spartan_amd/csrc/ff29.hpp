@@ -135,6 +135,47 @@ DEV void f29_redc_sum(F29& r, const F29* const (&a)[NP], const F29* const (&b)[N
     for (int i = 0; i < 14; ++i) r.v[i] = t[i];
 }
 
+// r = REDC(a0 b0 + a1 b1 + a2 b2 + a3 b3): one reduction for four products. A column then holds up
+// to 4 x 14 products and 14 m p terms, which can pass 2^64, so it is summed in two 64-bit chains
+// (A: products 0, 1; B: products 2, 3 and m p), each below 2^64 as long as every product is below
+// 2^59 (limbs < 2^29, or one factor's limbs < 2^30 as in the borrow-free lane-pair operands):
+// A <= 28 x 2^59, B <= 28 x 2^59 + 14 x 2^58. The chains are joined without a 65-bit sum: the column's
+// low 29 bits come from the low parts, the carry from the high parts plus the low parts' overflow.
+DEV void f29_redc_sum4(F29& r, const F29& a0, const F29& b0, const F29& a1, const F29& b1, const F29& a2,
+                       const F29& b2, const F29& a3, const F29& b3) {
+    uint32_t m[14], t[14];
+    uint64_t carry = 0;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+        const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+        uint64_t ca = 0, cb = 0;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            ca += (uint64_t)a0.v[i] * b0.v[k - i];
+            ca += (uint64_t)a1.v[i] * b1.v[k - i];
+            cb += (uint64_t)a2.v[i] * b2.v[k - i];
+            cb += (uint64_t)a3.v[i] * b3.v[k - i];
+        }
+#pragma unroll
+        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) cb += (uint64_t)m[i] * Q29::P[k - i];
+        ca = f29_opaque(ca);
+        cb = f29_opaque(cb);
+        // low: < 3 x 2^29 (+ m p0 < 2^58 below); high: < 2^36 each
+        uint64_t low = (ca & Q29::M) + (cb & Q29::M) + (carry & Q29::M);
+        const uint64_t high = (ca >> 29) + (cb >> 29) + (carry >> 29);
+        if (k < 14) {
+            m[k] = ((uint32_t)low * Q29::PINV) & Q29::M;
+            low += (uint64_t)m[k] * Q29::P[0];
+        } else {
+            t[k - 14] = (uint32_t)low & Q29::M;
+        }
+        carry = high + (low >> 29);
+    }
+    t[13] = (uint32_t)carry;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) r.v[i] = t[i];
+}
+
 // r = REDC(a b) = a b / 2^406 mod p, < 2p for inputs < 2^392
 DEV void f29_mul(F29& r, const F29& a, const F29& b) {
     const F29* const pa[1] = {&a};
@@ -292,6 +333,8 @@ struct Ops29;
 template <>
 struct Ops29<F29> {
     static DEV void mul(F29& r, const F29& a, const F29& b) { f29_mul(r, a, b); }
+    // r = a b + c d with one reduction (operands < 16p: the sum < 512 p^2 < 2^406 p), < 2p
+    static DEV void mul_sum(F29& r, const F29& a, const F29& b, const F29& c, const F29& d) { f29_mul2(r, a, b, c, d); }
     static DEV void sqr(F29& r, const F29& a) { f29_mul(r, a, a); }
     static DEV void add(F29& r, const F29& a, const F29& b) { f29_add(r, a, b); }
     template <int K>
@@ -319,6 +362,13 @@ struct Ops29<F29> {
 template <>
 struct Ops29<F2_29> {
     static DEV void mul(F2_29& r, const F2_29& a, const F2_29& b) { f2_29_mul(r, a, b); }
+    static DEV void mul_sum(F2_29& r, const F2_29& a, const F2_29& b, const F2_29& c, const F2_29& d) {
+        F2_29 x, y;
+        f2_29_mul(x, a, b);
+        f2_29_mul(y, c, d);
+        f29_add(r.c0, x.c0, y.c0);  // < 4p
+        f29_add(r.c1, x.c1, y.c1);
+    }
     static DEV void sqr(F2_29& r, const F2_29& a) { f2_29_sqr(r, a); }
     static DEV void add(F2_29& r, const F2_29& a, const F2_29& b) {
         f29_add(r.c0, a.c0, b.c0);

@@ -94,6 +94,32 @@ struct PairOps {
             f29_mul2(r.v, a.v, y1, ap, y2);
         }
     }
+    // r = a b + c d. Borrow-free form: one REDC of the lane's four products (f29_redc_sum4), < 2p;
+    // otherwise two products and an addition, < 4p
+    static DEV void mul_sum(P& r, const P& a, const P& b, const P& c, const P& d) {
+        if constexpr (kBorrowFree) {
+            const bool odd = pair_odd();
+            const uint32_t msk = odd ? 0u : 0xffffffffu;
+            F29 ap, y1, y2, cp, z1, z2;
+#pragma unroll
+            for (int i = 0; i < 14; ++i) {
+                ap.v[i] = pair_swap(a.v.v[i]);
+                y1.v[i] = pair_even(b.v.v[i]);
+                const uint32_t yb = pair_odd_val(b.v.v[i]);
+                y2.v[i] = (yb ^ msk) + (msk & (k16(i) + 1u));
+                cp.v[i] = pair_swap(c.v.v[i]);
+                z1.v[i] = pair_even(d.v.v[i]);
+                const uint32_t zd = pair_odd_val(d.v.v[i]);
+                z2.v[i] = (zd ^ msk) + (msk & (k16(i) + 1u));
+            }
+            f29_redc_sum4(r.v, a.v, y1, ap, y2, c.v, z1, cp, z2);
+        } else {
+            P x, y;
+            mul(x, a, b);
+            mul(y, c, d);
+            f29_add(r.v, x.v, y.v);
+        }
+    }
     // (a0 + a1)(a0 - a1 + KB p) on the even lane, (a0 + a0) a1 on the odd one; KB bounds c1
     template <int KB>
     static DEV void sqr_b(P& r, const P& a) {

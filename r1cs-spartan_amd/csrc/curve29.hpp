@@ -94,11 +94,17 @@ DEV void x29_from_aff_dbl(X29<F>& r, const F& ax, const F& ay) {
     O::add(s2, S, S);      // < 4p
     O::template sub<4>(r.x, t, s2);  // < 6p
     O::template reduce<8>(r.x);      // < 2p
-    O::template sub<2>(t, S, r.x);   // < 4p
-    O::mul(t, M, t);                 // < 2p
-    O::mul(s2, W, ay);               // < 2p
-    O::template sub<2>(r.y, t, s2);  // < 4p
-    O::template reduce<4>(r.y);
+    O::template sub<2>(t, S, r.x);  // < 4p
+    if constexpr (O::kFusedSum) {   // M t + (2p - W) ay in one reduction, < 2p
+        O::zero(s2);
+        O::template sub<2>(s2, s2, W);
+        O::mul_sum(r.y, M, t, s2, ay);
+    } else {
+        O::mul(t, M, t);                 // < 2p
+        O::mul(s2, W, ay);               // < 2p
+        O::template sub<2>(r.y, t, s2);  // < 4p
+        O::template reduce<4>(r.y);
+    }
     r.zz = V;
     r.zzz = W;
 }
@@ -122,10 +128,16 @@ DEV void x29_dbl(X29<F>& p) {
     O::template sub<4>(x3, t, s2);
     O::template reduce<8>(x3);
     O::template sub<2>(t, S, x3);
-    O::mul(t, M, t);
-    O::mul(s2, W, p.y);
-    O::template sub<2>(p.y, t, s2);
-    O::template reduce<4>(p.y);
+    if constexpr (O::kFusedSum) {  // M t + (2p - W) Y in one reduction, < 2p
+        O::zero(s2);
+        O::template sub<2>(s2, s2, W);
+        O::mul_sum(p.y, M, t, s2, p.y);
+    } else {
+        O::mul(t, M, t);
+        O::mul(s2, W, p.y);
+        O::template sub<2>(p.y, t, s2);
+        O::template reduce<4>(p.y);
+    }
     p.x = x3;
     O::mul(p.zz, V, p.zz);
     O::mul(p.zzz, W, p.zzz);
@@ -216,10 +228,17 @@ DEV void x29_add(X29<F>& p, const X29<F>& q) {
     O::template sub<4>(w, w, t);
     O::template reduce<8>(w);
     O::template sub<2>(t, Q, w);
-    O::mul(t, R, t);
-    O::mul(S1, S1, PPP);
-    O::template sub<2>(p.y, t, S1);
-    O::template reduce<4>(p.y);
+    if constexpr (O::kFusedSum) {  // R t + (2p - S1) PPP in one reduction, < 2p
+        F n;
+        O::zero(n);
+        O::template sub<2>(n, n, S1);
+        O::mul_sum(p.y, R, t, n, PPP);
+    } else {
+        O::mul(t, R, t);
+        O::mul(S1, S1, PPP);
+        O::template sub<2>(p.y, t, S1);
+        O::template reduce<4>(p.y);
+    }
     p.x = w;
     O::mul(t, p.zz, q.zz);
     O::mul(p.zz, t, PP);

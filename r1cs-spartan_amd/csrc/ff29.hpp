@@ -332,6 +332,7 @@ template <class F>
 struct Ops29;
 template <>
 struct Ops29<F29> {
+    static constexpr bool kFusedSum = true;  // mul_sum is one reduction
     static DEV void mul(F29& r, const F29& a, const F29& b) { f29_mul(r, a, b); }
     // r = a b + c d with one reduction (operands < 16p: the sum < 512 p^2 < 2^406 p), < 2p
     static DEV void mul_sum(F29& r, const F29& a, const F29& b, const F29& c, const F29& d) { f29_mul2(r, a, b, c, d); }
@@ -361,6 +362,7 @@ struct Ops29<F29> {
 };
 template <>
 struct Ops29<F2_29> {
+    static constexpr bool kFusedSum = false;
     static DEV void mul(F2_29& r, const F2_29& a, const F2_29& b) { f2_29_mul(r, a, b); }
     static DEV void mul_sum(F2_29& r, const F2_29& a, const F2_29& b, const F2_29& c, const F2_29& d) {
         F2_29 x, y;

@@ -71,6 +71,7 @@ struct FP29A {
 
 template <class P, bool kBorrowFree>
 struct PairOps {
+    static constexpr bool kFusedSum = kBorrowFree;
     static DEV void mul(P& r, const P& a, const P& b) {
         const bool odd = pair_odd();
         if constexpr (kBorrowFree) {

@@ -48,7 +48,14 @@ struct Acc<Fq> {
 template <>
 struct Acc<Fq2> {
     using Pt = Aff<Fq2>;  // 192 bytes: 1.5 lines, the lane pair's halves 96 bytes each
+#ifndef SPX_G2_WEIGHT_BORROW_FREE
+#define SPX_G2_WEIGHT_BORROW_FREE 0
+#endif
+#if SPX_G2_WEIGHT_BORROW_FREE
+    using T = FP29A;
+#else
     using T = FP29;
+#endif
     using TA = FP29A;  // borrow-free operand preparation in the accumulation only (fq2pair.hpp)
     static constexpr int kLanes = 2, kWaves = SPX_G2_WAVES;
     static DEV void ld_raw(AffRaw& a, const Aff<Fq2>* p) {

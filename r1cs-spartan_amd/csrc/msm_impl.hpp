@@ -91,6 +91,114 @@ struct Acc<Fq2> {
         fp29_st(&p->zzz, r.zzz);
     }
 };
+
+// ---- quads: two lane pairs per G2 element, for the latency-bound weighting and partial kernels.
+// Both pairs hold the same operands; x29_add_quad splits the products of add-2008-s between them
+// (A = lanes 4k, 4k+1; B = lanes 4k+2, 4k+3) and exchanges results through DPP quad_perm [2,3,0,1]:
+// 7 products on the dependent path instead of 14, so one addition's latency (the whole cost of the
+// weighting tree's upper levels) roughly halves. Both pairs end with the identical sum.
+DEV bool quad_half() { return (__lane_id() & 2) != 0; }
+DEV uint32_t quad_swap(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+DEV FP29 quad_swap(const FP29& a) {
+    FP29 r;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) r.v.v[i] = quad_swap(a.v.v[i]);
+    return r;
+}
+// h ? b : a (h: this lane is in the quad's B pair)
+DEV FP29 quad_sel(bool h, const FP29& a, const FP29& b) {
+    FP29 r;
+    r.v = f29_select(h, b.v, a.v);
+    return r;
+}
+
+// p += q; p and q identical on both pairs of the quad; inputs and output as x29_add (< 2p, X may be
+// loose < 8p, Y < 4p on input)
+DEV void x29_add_quad(X29<FP29>& p, const X29<FP29>& q) {
+    using O = Ops29<FP29>;
+    if (x29_is_inf(q)) return;
+    if (x29_is_inf(p)) {
+        p = q;
+        return;
+    }
+    const bool h = quad_half();
+    // A: U1 = X1 ZZ2, S1 = Y1 ZZZ2, ZZ1 ZZ2;  B: U2 = X2 ZZ1, S2 = Y2 ZZZ1, ZZZ1 ZZZ2
+    FP29 u, s, z;
+    O::mul(u, quad_sel(h, p.x, q.x), quad_sel(h, q.zz, p.zz));
+    O::mul(s, quad_sel(h, p.y, q.y), quad_sel(h, q.zzz, p.zzz));
+    O::mul(z, quad_sel(h, p.zz, p.zzz), quad_sel(h, q.zz, q.zzz));
+    const FP29 uo = quad_swap(u), so = quad_swap(s), zo = quad_swap(z);
+    const FP29 U1 = quad_sel(h, u, uo), U2 = quad_sel(h, uo, u);
+    const FP29 S1 = quad_sel(h, s, so), S2 = quad_sel(h, so, s);
+    const FP29 ZZ12 = quad_sel(h, z, zo), ZZZ12 = quad_sel(h, zo, z);
+    FP29 P, R;
+    O::template sub<2>(P, U2, U1);
+    O::template sub<2>(R, S2, S1);
+    if (O::template zero_lt<4>(P)) {  // pair predicates on identical values: the quad branches together
+        if (O::template zero_lt<4>(R))
+            x29_dbl(p);
+        else
+            x29_set_inf(p);
+        return;
+    }
+    // A: PP = P^2;  B: T = R^2  (P, R < 4p)
+    FP29 sq;
+    O::sqr(sq, quad_sel(h, P, R));
+    const FP29 sqo = quad_swap(sq);
+    const FP29 PP = quad_sel(h, sq, sqo), T = quad_sel(h, sqo, sq);
+    // A: PPP = P PP;  B: Q = U1 PP
+    FP29 m3;
+    O::mul(m3, quad_sel(h, P, U1), PP);
+    const FP29 m3o = quad_swap(m3);
+    const FP29 PPP = quad_sel(h, m3, m3o), Q = quad_sel(h, m3o, m3);
+    FP29 w, t;
+    O::template sub<2>(w, T, PPP);
+    O::add(t, Q, Q);
+    O::template sub<4>(w, w, t);
+    O::template reduce<8>(w);       // X3 < 2p
+    O::template sub<2>(t, Q, w);    // < 4p
+    // A: R t, ZZ1 ZZ2 PP;  B: S1 PPP, ZZZ1 ZZZ2 PPP
+    FP29 y4, z4;
+    O::mul(y4, quad_sel(h, R, S1), quad_sel(h, t, PPP));
+    O::mul(z4, quad_sel(h, ZZ12, ZZZ12), quad_sel(h, PP, PPP));
+    const FP29 y4o = quad_swap(y4), z4o = quad_swap(z4);
+    O::template sub<2>(p.y, quad_sel(h, y4, y4o), quad_sel(h, y4o, y4));  // R t - S1 PPP
+    O::template reduce<4>(p.y);
+    p.x = w;
+    p.zz = quad_sel(h, z4, z4o);
+    p.zzz = quad_sel(h, z4o, z4);
+}
+
+#ifndef SPX_G2_QUAD
+#define SPX_G2_QUAD 1
+#endif
+// lanes per element in the weighting / partial kernels (G2: a quad when SPX_G2_QUAD)
+template <class F>
+struct TreeLanes {
+    static constexpr int v = Acc<F>::kLanes;
+};
+template <>
+struct TreeLanes<Fq2> {
+    static constexpr int v = SPX_G2_QUAD ? 4 : 2;
+};
+template <class F>
+DEV void tree_add(X29<typename Acc<F>::T>& p, const X29<typename Acc<F>::T>& q) {
+    if constexpr (TreeLanes<F>::v == 4)
+        x29_add_quad(p, q);
+    else
+        x29_add(p, q);
+}
+template <class F>
+DEV uint64_t tree_elem() {
+    return (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / TreeLanes<F>::v;
+}
+template <class F>
+static unsigned tree_blocks(uint64_t elems) {
+    return (unsigned)((elems * TreeLanes<F>::v + kHeavy - 1) / kHeavy);
+}
+
 // element index of the calling lane (one element per Acc<F>::kLanes lanes)
 template <class F>
 DEV uint64_t acc_elem() {
@@ -172,7 +280,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uin
                                                                        Xyzz<F>* __restrict__ out) {
     using A = Acc<F>;
     using T = typename A::T;
-    const uint32_t s = (uint32_t)acc_elem<F>();
+    const uint32_t s = (uint32_t)tree_elem<F>();
     if (s >= segoff[nb]) return;
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
@@ -183,7 +291,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uin
     for (uint32_t e = start + 1; e < end; ++e) {
         X29<T> p;
         A::ld(p, in + e);
-        x29_add(acc, p);
+        tree_add<F>(acc, p);
     }
     A::st(out + s, acc);
 }
@@ -209,7 +317,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, const Xyzz<F>* __restrict__ P,
     Xyzz<F>* __restrict__ Fo, Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
     using A = Acc<F>;
-    const uint64_t t = acc_elem<F>();
+    const uint64_t t = tree_elem<F>();
     if (t >= wp[ninst]) return;
     const int i = find_slot(wp, ninst, t);
     const uint32_t k = (uint32_t)(t - wp[i]);
@@ -240,7 +348,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
             A::ld(a, Fo + o);
             b = run;
         }
-        x29_add(a, b);
+        tree_add<F>(a, b);
         if (bucket_step) {
             run = a;
         } else {
@@ -260,7 +368,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
     const Xyzz<F>* __restrict__ Fi, const Xyzz<F>* __restrict__ Si, const Xyzz<F>* __restrict__ Di,
     Xyzz<F>* __restrict__ Fo, Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
     using A = Acc<F>;
-    const uint64_t t = acc_elem<F>();
+    const uint64_t t = tree_elem<F>();
     const uint64_t N = wp[ninst];
     if (t >= 3 * N) return;
     const uint32_t comp = (uint32_t)(t / N);
@@ -274,23 +382,23 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
         A::ld(a, Fi + base + 2 * k);
         if (has_r) {
             A::ld(b, Di + base + 2 * k + 1);
-            x29_add(a, b);
+            tree_add<F>(a, b);
             A::ld(b, Fi + base + 2 * k + 1);
-            x29_add(a, b);
+            tree_add<F>(a, b);
         }
         A::st(Fo + base + k, a);
     } else if (comp == 1) {
         A::ld(a, Si + base + 2 * k);
         if (has_r) {
             A::ld(b, Si + base + 2 * k + 1);
-            x29_add(a, b);
+            tree_add<F>(a, b);
         }
         A::st(So + base + k, a);
     } else {
         A::ld(a, Di + base + 2 * k);
         if (has_r) {
             A::ld(b, Di + base + 2 * k + 1);
-            x29_add(a, b);
+            tree_add<F>(a, b);
         }
         x29_dbl(a);
         A::st(Do + base + k, a);
@@ -349,7 +457,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
         exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
-        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(acc_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur_cnt,
+        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur_cnt,
                            cur, nxt);
         kp_end((double)(cur_max_segs + nsegs) * psz, s, (double)cur_max_segs);
         std::swap(cur, nxt);
@@ -401,12 +509,12 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     {
         uint64_t work = wp[ninst];
-        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(acc_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, ninst, d_noff,
+        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, ninst, d_noff,
                            cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
     }
     for (int lv = 1; lv <= levels; ++lv) {
         uint64_t work = 3 * wp[(size_t)lv * (ninst + 1) + ninst];
-        hipLaunchKernelGGL(k_tree_level<F>, dim3(acc_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (ninst + 1),
+        hipLaunchKernelGGL(k_tree_level<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (ninst + 1),
                            ninst, d_noff, d_cin + (size_t)lv * ninst, A3[0], A3[1], A3[2], B3[0], B3[1], B3[2]);
         std::swap(A3, B3);
     }

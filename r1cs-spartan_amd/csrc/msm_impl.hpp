@@ -114,6 +114,43 @@ DEV FP29 quad_sel(bool h, const FP29& a, const FP29& b) {
     return r;
 }
 
+// 2p (dbl-2008-s-1) split over the quad: 5 products on the dependent path instead of 9 (the pair
+// that would square M computes M M as a product, so both pairs run the same instruction stream)
+DEV void x29_dbl_quad(X29<FP29>& p) {
+    using O = Ops29<FP29>;
+    if (x29_is_inf(p)) return;
+    const bool h = quad_half();
+    FP29 U;
+    O::add(U, p.y, p.y);  // < 8p
+    FP29 s1;
+    O::sqr(s1, quad_sel(h, U, p.x));  // A: V = U^2, B: X2 = X^2 (c1 < 8p)
+    const FP29 s1o = quad_swap(s1);
+    const FP29 V = quad_sel(h, s1, s1o), X2 = quad_sel(h, s1o, s1);
+    FP29 M;
+    O::add(M, X2, X2);
+    O::add(M, M, X2);  // < 6p
+    FP29 a, b;
+    O::mul(a, quad_sel(h, U, M), quad_sel(h, V, M));       // A: W = U V,  B: T = M M
+    O::mul(b, quad_sel(h, p.x, V), quad_sel(h, V, p.zz));  // A: S = X V,  B: ZZ3 = V ZZ
+    const FP29 ao = quad_swap(a), bo = quad_swap(b);
+    const FP29 W = quad_sel(h, a, ao), T = quad_sel(h, ao, a);
+    const FP29 S = quad_sel(h, b, bo), ZZ3 = quad_sel(h, bo, b);
+    FP29 s2, x3, t2;
+    O::add(s2, S, S);                 // < 4p
+    O::template sub<4>(x3, T, s2);    // < 6p
+    O::template reduce<8>(x3);        // < 2p
+    O::template sub<2>(t2, S, x3);    // < 4p
+    FP29 c, d;
+    O::mul(c, quad_sel(h, M, W), quad_sel(h, t2, p.y));  // A: M (S - X3),  B: W Y
+    O::mul(d, W, p.zzz);                                  // ZZZ3, both pairs
+    const FP29 co = quad_swap(c);
+    O::template sub<2>(p.y, quad_sel(h, c, co), quad_sel(h, co, c));
+    O::template reduce<4>(p.y);
+    p.x = x3;
+    p.zz = ZZ3;
+    p.zzz = d;
+}
+
 // p += q; p and q identical on both pairs of the quad; inputs and output as x29_add (< 2p, X may be
 // loose < 8p, Y < 4p on input)
 DEV void x29_add_quad(X29<FP29>& p, const X29<FP29>& q) {
@@ -138,7 +175,7 @@ DEV void x29_add_quad(X29<FP29>& p, const X29<FP29>& q) {
     O::template sub<2>(R, S2, S1);
     if (O::template zero_lt<4>(P)) {  // pair predicates on identical values: the quad branches together
         if (O::template zero_lt<4>(R))
-            x29_dbl(p);
+            x29_dbl_quad(p);
         else
             x29_set_inf(p);
         return;
@@ -189,6 +226,13 @@ DEV void tree_add(X29<typename Acc<F>::T>& p, const X29<typename Acc<F>::T>& q) 
         x29_add_quad(p, q);
     else
         x29_add(p, q);
+}
+template <class F>
+DEV void tree_dbl(X29<typename Acc<F>::T>& p) {
+    if constexpr (TreeLanes<F>::v == 4)
+        x29_dbl_quad(p);
+    else
+        x29_dbl(p);
 }
 template <class F>
 DEV uint64_t tree_elem() {
@@ -358,7 +402,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     }
     A::st(So + o, run);
 #pragma unroll 1
-    for (uint32_t d = 0; d < lgm; ++d) x29_dbl(run);
+    for (uint32_t d = 0; d < lgm; ++d) tree_dbl<F>(run);
     A::st(Do + o, run);
 }
 
@@ -400,7 +444,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
             A::ld(b, Di + base + 2 * k + 1);
             tree_add<F>(a, b);
         }
-        x29_dbl(a);
+        tree_dbl<F>(a);
         A::st(Do + base + k, a);
     }
 }

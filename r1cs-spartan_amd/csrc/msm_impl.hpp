@@ -92,129 +92,147 @@ struct Acc<Fq2> {
     }
 };
 
-// ---- quads: two lane pairs per G2 element, for the latency-bound weighting and partial kernels.
-// Both pairs hold the same operands; x29_add_quad splits the products of add-2008-s between them
-// (A = lanes 4k, 4k+1; B = lanes 4k+2, 4k+3) and exchanges results through DPP quad_perm [2,3,0,1]:
-// 7 products on the dependent path instead of 14, so one addition's latency (the whole cost of the
-// weighting tree's upper levels) roughly halves. Both pairs end with the identical sum.
-DEV bool quad_half() { return (__lane_id() & 2) != 0; }
-DEV uint32_t quad_swap(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-}
-DEV FP29 quad_swap(const FP29& a) {
-    FP29 r;
+// ---- split additions for the latency-bound weighting and partial kernels: two lane groups hold the
+// same operands and split one addition's products (G2: two lane pairs = a quad, exchanged through DPP
+// quad_perm [2,3,0,1]; G1: two lanes, exchanged through quad_perm [1,0,3,2]). 7 products on the
+// dependent path of an addition instead of 14, 5 instead of 9 for a doubling, so one addition's
+// latency (the whole cost of the weighting tree's upper levels) roughly halves. Both groups end with
+// the identical result; group A = the lower, B = the upper.
+template <class T>
+struct Split;
+template <>
+struct Split<FP29> {
+    static DEV bool half() { return (__lane_id() & 2) != 0; }
+    static DEV FP29 swap(const FP29& a) {
+        FP29 r;
 #pragma unroll
-    for (int i = 0; i < 14; ++i) r.v.v[i] = quad_swap(a.v.v[i]);
-    return r;
-}
-// h ? b : a (h: this lane is in the quad's B pair)
-DEV FP29 quad_sel(bool h, const FP29& a, const FP29& b) {
-    FP29 r;
-    r.v = f29_select(h, b.v, a.v);
-    return r;
-}
+        for (int i = 0; i < 14; ++i)
+            r.v.v[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v.v[i], 0x4E, 0xF, 0xF, false);
+        return r;
+    }
+    static DEV FP29 sel(bool h, const FP29& a, const FP29& b) {  // h ? b : a
+        FP29 r;
+        r.v = f29_select(h, b.v, a.v);
+        return r;
+    }
+};
+template <>
+struct Split<F29> {
+    static DEV bool half() { return pair_odd(); }
+    static DEV F29 swap(const F29& a) { return pair_swap(a); }
+    static DEV F29 sel(bool h, const F29& a, const F29& b) { return f29_select(h, b, a); }
+};
 
-// 2p (dbl-2008-s-1) split over the quad: 5 products on the dependent path instead of 9 (the pair
-// that would square M computes M M as a product, so both pairs run the same instruction stream)
-DEV void x29_dbl_quad(X29<FP29>& p) {
-    using O = Ops29<FP29>;
+// 2p (dbl-2008-s-1) split over two groups (the group that would square M computes M M as a
+// product, so both groups run the same instruction stream)
+template <class T>
+DEV void x29_dbl_split(X29<T>& p) {
+    using O = Ops29<T>;
+    using S2 = Split<T>;
     if (x29_is_inf(p)) return;
-    const bool h = quad_half();
-    FP29 U;
+    const bool h = S2::half();
+    T U;
     O::add(U, p.y, p.y);  // < 8p
-    FP29 s1;
-    O::sqr(s1, quad_sel(h, U, p.x));  // A: V = U^2, B: X2 = X^2 (c1 < 8p)
-    const FP29 s1o = quad_swap(s1);
-    const FP29 V = quad_sel(h, s1, s1o), X2 = quad_sel(h, s1o, s1);
-    FP29 M;
+    T s1;
+    O::sqr(s1, S2::sel(h, U, p.x));  // A: V = U^2, B: X2 = X^2 (c1 < 8p)
+    const T s1o = S2::swap(s1);
+    const T V = S2::sel(h, s1, s1o), X2 = S2::sel(h, s1o, s1);
+    T M;
     O::add(M, X2, X2);
     O::add(M, M, X2);  // < 6p
-    FP29 a, b;
-    O::mul(a, quad_sel(h, U, M), quad_sel(h, V, M));       // A: W = U V,  B: T = M M
-    O::mul(b, quad_sel(h, p.x, V), quad_sel(h, V, p.zz));  // A: S = X V,  B: ZZ3 = V ZZ
-    const FP29 ao = quad_swap(a), bo = quad_swap(b);
-    const FP29 W = quad_sel(h, a, ao), T = quad_sel(h, ao, a);
-    const FP29 S = quad_sel(h, b, bo), ZZ3 = quad_sel(h, bo, b);
-    FP29 s2, x3, t2;
+    T a, b;
+    O::mul(a, S2::sel(h, U, M), S2::sel(h, V, M));       // A: W = U V,  B: T = M M
+    O::mul(b, S2::sel(h, p.x, V), S2::sel(h, V, p.zz));  // A: S = X V,  B: ZZ3 = V ZZ
+    const T ao = S2::swap(a), bo = S2::swap(b);
+    const T W = S2::sel(h, a, ao), Tm = S2::sel(h, ao, a);
+    const T S = S2::sel(h, b, bo), ZZ3 = S2::sel(h, bo, b);
+    T s2, x3, t2;
     O::add(s2, S, S);                 // < 4p
-    O::template sub<4>(x3, T, s2);    // < 6p
+    O::template sub<4>(x3, Tm, s2);   // < 6p
     O::template reduce<8>(x3);        // < 2p
     O::template sub<2>(t2, S, x3);    // < 4p
-    FP29 c, d;
-    O::mul(c, quad_sel(h, M, W), quad_sel(h, t2, p.y));  // A: M (S - X3),  B: W Y
-    O::mul(d, W, p.zzz);                                  // ZZZ3, both pairs
-    const FP29 co = quad_swap(c);
-    O::template sub<2>(p.y, quad_sel(h, c, co), quad_sel(h, co, c));
+    T c, d;
+    O::mul(c, S2::sel(h, M, W), S2::sel(h, t2, p.y));  // A: M (S - X3),  B: W Y
+    O::mul(d, W, p.zzz);                                // ZZZ3, both groups
+    const T co = S2::swap(c);
+    O::template sub<2>(p.y, S2::sel(h, c, co), S2::sel(h, co, c));
     O::template reduce<4>(p.y);
     p.x = x3;
     p.zz = ZZ3;
     p.zzz = d;
 }
 
-// p += q; p and q identical on both pairs of the quad; inputs and output as x29_add (< 2p, X may be
-// loose < 8p, Y < 4p on input)
-DEV void x29_add_quad(X29<FP29>& p, const X29<FP29>& q) {
-    using O = Ops29<FP29>;
+// p += q (add-2008-s) split over two groups; p and q identical on both; inputs and output as x29_add
+// (< 2p, X may be loose < 8p, Y < 4p on input)
+template <class T>
+DEV void x29_add_split(X29<T>& p, const X29<T>& q) {
+    using O = Ops29<T>;
+    using S2 = Split<T>;
     if (x29_is_inf(q)) return;
     if (x29_is_inf(p)) {
         p = q;
         return;
     }
-    const bool h = quad_half();
+    const bool h = S2::half();
     // A: U1 = X1 ZZ2, S1 = Y1 ZZZ2, ZZ1 ZZ2;  B: U2 = X2 ZZ1, S2 = Y2 ZZZ1, ZZZ1 ZZZ2
-    FP29 u, s, z;
-    O::mul(u, quad_sel(h, p.x, q.x), quad_sel(h, q.zz, p.zz));
-    O::mul(s, quad_sel(h, p.y, q.y), quad_sel(h, q.zzz, p.zzz));
-    O::mul(z, quad_sel(h, p.zz, p.zzz), quad_sel(h, q.zz, q.zzz));
-    const FP29 uo = quad_swap(u), so = quad_swap(s), zo = quad_swap(z);
-    const FP29 U1 = quad_sel(h, u, uo), U2 = quad_sel(h, uo, u);
-    const FP29 S1 = quad_sel(h, s, so), S2 = quad_sel(h, so, s);
-    const FP29 ZZ12 = quad_sel(h, z, zo), ZZZ12 = quad_sel(h, zo, z);
-    FP29 P, R;
+    T u, s, z;
+    O::mul(u, S2::sel(h, p.x, q.x), S2::sel(h, q.zz, p.zz));
+    O::mul(s, S2::sel(h, p.y, q.y), S2::sel(h, q.zzz, p.zzz));
+    O::mul(z, S2::sel(h, p.zz, p.zzz), S2::sel(h, q.zz, q.zzz));
+    const T uo = S2::swap(u), so = S2::swap(s), zo = S2::swap(z);
+    const T U1 = S2::sel(h, u, uo), U2 = S2::sel(h, uo, u);
+    const T Sa = S2::sel(h, s, so), Sb = S2::sel(h, so, s);
+    const T ZZ12 = S2::sel(h, z, zo), ZZZ12 = S2::sel(h, zo, z);
+    T P, R;
     O::template sub<2>(P, U2, U1);
-    O::template sub<2>(R, S2, S1);
-    if (O::template zero_lt<4>(P)) {  // pair predicates on identical values: the quad branches together
+    O::template sub<2>(R, Sb, Sa);
+    if (O::template zero_lt<4>(P)) {  // identical values on both groups: they branch together
         if (O::template zero_lt<4>(R))
-            x29_dbl_quad(p);
+            x29_dbl_split(p);
         else
             x29_set_inf(p);
         return;
     }
     // A: PP = P^2;  B: T = R^2  (P, R < 4p)
-    FP29 sq;
-    O::sqr(sq, quad_sel(h, P, R));
-    const FP29 sqo = quad_swap(sq);
-    const FP29 PP = quad_sel(h, sq, sqo), T = quad_sel(h, sqo, sq);
+    T sq;
+    O::sqr(sq, S2::sel(h, P, R));
+    const T sqo = S2::swap(sq);
+    const T PP = S2::sel(h, sq, sqo), Tr = S2::sel(h, sqo, sq);
     // A: PPP = P PP;  B: Q = U1 PP
-    FP29 m3;
-    O::mul(m3, quad_sel(h, P, U1), PP);
-    const FP29 m3o = quad_swap(m3);
-    const FP29 PPP = quad_sel(h, m3, m3o), Q = quad_sel(h, m3o, m3);
-    FP29 w, t;
-    O::template sub<2>(w, T, PPP);
+    T m3;
+    O::mul(m3, S2::sel(h, P, U1), PP);
+    const T m3o = S2::swap(m3);
+    const T PPP = S2::sel(h, m3, m3o), Q = S2::sel(h, m3o, m3);
+    T w, t;
+    O::template sub<2>(w, Tr, PPP);
     O::add(t, Q, Q);
     O::template sub<4>(w, w, t);
     O::template reduce<8>(w);       // X3 < 2p
     O::template sub<2>(t, Q, w);    // < 4p
     // A: R t, ZZ1 ZZ2 PP;  B: S1 PPP, ZZZ1 ZZZ2 PPP
-    FP29 y4, z4;
-    O::mul(y4, quad_sel(h, R, S1), quad_sel(h, t, PPP));
-    O::mul(z4, quad_sel(h, ZZ12, ZZZ12), quad_sel(h, PP, PPP));
-    const FP29 y4o = quad_swap(y4), z4o = quad_swap(z4);
-    O::template sub<2>(p.y, quad_sel(h, y4, y4o), quad_sel(h, y4o, y4));  // R t - S1 PPP
+    T y4, z4;
+    O::mul(y4, S2::sel(h, R, Sa), S2::sel(h, t, PPP));
+    O::mul(z4, S2::sel(h, ZZ12, ZZZ12), S2::sel(h, PP, PPP));
+    const T y4o = S2::swap(y4), z4o = S2::swap(z4);
+    O::template sub<2>(p.y, S2::sel(h, y4, y4o), S2::sel(h, y4o, y4));  // R t - S1 PPP
     O::template reduce<4>(p.y);
     p.x = w;
-    p.zz = quad_sel(h, z4, z4o);
-    p.zzz = quad_sel(h, z4o, z4);
+    p.zz = S2::sel(h, z4, z4o);
+    p.zzz = S2::sel(h, z4o, z4);
 }
 
 #ifndef SPX_G2_QUAD
 #define SPX_G2_QUAD 1
 #endif
-// lanes per element in the weighting / partial kernels (G2: a quad when SPX_G2_QUAD)
+#ifndef SPX_G1_SPLIT
+#define SPX_G1_SPLIT 1
+#endif
+// lanes per element in the weighting / partial kernels: G2 a quad, G1 a pair (split additions)
 template <class F>
-struct TreeLanes {
-    static constexpr int v = Acc<F>::kLanes;
+struct TreeLanes;
+template <>
+struct TreeLanes<Fq> {
+    static constexpr int v = SPX_G1_SPLIT ? 2 : 1;
 };
 template <>
 struct TreeLanes<Fq2> {
@@ -222,15 +240,15 @@ struct TreeLanes<Fq2> {
 };
 template <class F>
 DEV void tree_add(X29<typename Acc<F>::T>& p, const X29<typename Acc<F>::T>& q) {
-    if constexpr (TreeLanes<F>::v == 4)
-        x29_add_quad(p, q);
+    if constexpr (TreeLanes<F>::v == 2 * Acc<F>::kLanes)
+        x29_add_split(p, q);
     else
         x29_add(p, q);
 }
 template <class F>
 DEV void tree_dbl(X29<typename Acc<F>::T>& p) {
-    if constexpr (TreeLanes<F>::v == 4)
-        x29_dbl_quad(p);
+    if constexpr (TreeLanes<F>::v == 2 * Acc<F>::kLanes)
+        x29_dbl_split(p);
     else
         x29_dbl(p);
 }

@@ -213,11 +213,18 @@ def kernel_stats(spx, L, hctx, per_proof_div):
 
 def roofline_valu(stats, dom):
     """dominant MSM kernel: VALU issue (SQ_INSTS_VALU per launch from the committed PMC pass) over the
-    live HIP-event launch duration, against the chip's VALU issue peak; HBM side as secondary fields."""
+    live HIP-event launch duration, against the chip's VALU issue peak; HBM side as secondary fields.
+    The PMC pass is one whole proof on one rank; a proof sharded over G ranks gives each rank's launches
+    part of its references, so the per-launch counters are scaled by this run's algorithmic bytes per
+    launch over the profiled run's (pmc_kernels.json alg_bytes_per_launch)."""
     d = stats[dom]
     avg_s = d["ms"] / d["launches"] / 1e3
     per_launch = d["bytes"] / d["launches"]
-    pm = pmc_kernel(dom) or {}
+    pm = dict(pmc_kernel(dom) or {})
+    share = per_launch / pm["alg_bytes_per_launch"] if pm.get("alg_bytes_per_launch") else 1.0
+    for key in ("SQ_INSTS_VALU_per_launch", "traffic_bytes"):
+        if pm.get(key):
+            pm[key] *= share
     insts = pm.get("SQ_INSTS_VALU_per_launch")
     roof = {
         "kernel": KSYM.get(dom, dom),
@@ -230,6 +237,7 @@ def roofline_valu(stats, dom):
         "avg_launch_us": round(avg_s * 1e6, 2),
         "valu_insts_per_launch": insts,
         "valu_source": "profiles/pmc_kernels.json (rocprofv3 --pmc SQ_INSTS_VALU, one proof in flight, same build)",
+        "pmc_share": round(share, 4),
         "note": "integer big-number VALU work (v_mad_u64_u32 limb products), no MFMA; live HIP-event duration with "
         "one proof at a time",
     }

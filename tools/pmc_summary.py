@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--calib-fetch")
     ap.add_argument("--calib-write")
     ap.add_argument("--valu")
+    ap.add_argument("--bench", help="bench.py JSON of a run with the same launch mix (its roofline kernel's "
+                    "algorithmic bytes per launch are recorded, so a run with smaller launches can scale the counters)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     unit = 1024.0  # KiB
@@ -110,6 +112,14 @@ def main():
             for c, (tot, n) in cs.items():
                 rec[c + "_per_launch"] = tot / n if n else None
                 rec["launches_valu_pass"] = n
+    if a.bench:
+        try:
+            rf = json.loads(open(a.bench).read().strip().splitlines()[-1]).get("roofline") or {}
+            alg = (rf.get("hbm") or {}).get("algorithmic_bytes_per_launch")
+            if alg and rf.get("kernel") in out["kernels"]:
+                out["kernels"][rf["kernel"]]["alg_bytes_per_launch"] = alg
+        except (OSError, ValueError, IndexError):
+            pass
     json.dump(out, open(a.out, "w"), indent=1)
     print("wrote", a.out, len(out["kernels"]), "kernels")
 

@@ -44,5 +44,5 @@ echo "valu done" >&2
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d "$RAW/cfetch" -o run --output-format csv -- "$ROOT/tools/calib_stream" > "$OUT/calib.txt" 2>&1
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d "$RAW/cwrite" -o run --output-format csv -- "$ROOT/tools/calib_stream" >> "$OUT/calib.txt" 2>&1
 python3 "$ROOT/tools/pmc_summary.py" --fetch "$RAW/fetch" --write "$RAW/write" --calib-fetch "$RAW/cfetch" \
-    --calib-write "$RAW/cwrite" --valu "$RAW/valu" --out "$OUT/pmc_kernels.json"
+    --calib-write "$RAW/cwrite" --valu "$RAW/valu" --bench "$OUT/bench_traced_inflight1.json" --out "$OUT/pmc_kernels.json"
 echo "profile done: $OUT" >&2

@@ -12,7 +12,7 @@
 
 namespace spx {
 
-static constexpr uint32_t kSeg1Default = 32;  // references per thread, affine accumulation level
+static constexpr uint32_t kSeg1Default = 64;  // references per thread, affine accumulation level (A/B: profiles/r02_ab19_seg.jsonl, r02_ab20_seg.jsonl)
 uint32_t seg1_len(bool g2);                      // kSeg1Default unless SPX_KSEG1 / SPX_KSEG1_G2 (tuning)
 // seg1 lowered so the accumulation grid fills whole rounds of resident waves (no near-empty last round)
 uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem);

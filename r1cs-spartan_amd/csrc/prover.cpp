@@ -38,8 +38,17 @@ Ctx::Ctx(int dev) : device(dev) {
     msm = msm_ws_create();
     comm.reset(new LocalComm());
 }
+void Ctx::ensure_side() {
+    if (side) return;
+    SPX_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    SPX_HIP(hipEventCreateWithFlags(&side_ev, hipEventDisableTiming));
+    msm_side = msm_ws_create();
+}
 Ctx::~Ctx() {
     (void)hipSetDevice(device);
+    if (msm_side) msm_ws_destroy(msm_side);
+    if (side_ev) (void)hipEventDestroy(side_ev);
+    if (side) (void)hipStreamDestroy(side);
     msm_ws_destroy(msm);
     scratch.release();
     if (pin) (void)hipHostFree(pin);
@@ -644,10 +653,24 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
 // launched right behind the commitment (before any challenge exists, overlapping the host's
 // absorption of the matrices) and handed to both open_z calls: a quarter of the proof's G2 work.
 static bool lvl0_local(int L, int G) { return L - ilog2((uint64_t)G) >= 1; }
-static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank) {
+// on_side: on the context's second stream (ordered after the main stream's work so far), without
+// kernel statistics (they time the main stream only)
+static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank, bool on_side = false) {
     const uint64_t half = ((1ull << L) / G) / 2;
+    hipStream_t st = C.stream;
+    MsmWorkspace* ws = C.msm;
+    struct KpRestore {
+        KProf* kp = g_kprof;
+        ~KpRestore() { g_kprof = kp; }
+    } restore;
+    if (on_side) {  // C.side_ev: recorded on the main stream once z is in place (prove)
+        SPX_HIP(hipStreamWaitEvent(C.side, C.side_ev, 0));
+        st = C.side;
+        ws = C.msm_side;
+        g_kprof = nullptr;
+    }
     Fr* q = C.buf<Fr>(Ctx::kSlotLvl0Q, 32 * half);
-    launch_open_level(z_local, nullptr, q, nullptr, half, C.stream);
+    launch_open_level(z_local, nullptr, q, nullptr, half, st);
     MsmInst I{};
     I.pts_off = P.g2_off[0] + (uint64_t)rank * half;
     I.stride = (uint32_t)(1ull << (L - 1));
@@ -657,11 +680,14 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank
     I.W = (uint32_t)P.g2_W[0];
     const size_t xb = 4 * sizeof(Fq2);
     void* out = C.buf(Ctx::kSlotLvl0Out, xb);
-    msm_run_g2(C.msm, &I, 1, P.g2_pre.as<G2Aff>(), q, out, C.stream);
-    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, xb, 4 << 10), out, xb, hipMemcpyDeviceToHost, C.stream));
+    msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st);
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, xb, 4 << 10), out, xb, hipMemcpyDeviceToHost, st));
 }
-static Affine<HFq2> lvl0_finish(Ctx& C, int G) {
-    C.sync();
+static Affine<HFq2> lvl0_finish(Ctx& C, int G, bool on_side = false) {
+    if (on_side)
+        SPX_HIP(hipStreamSynchronize(C.side));
+    else
+        C.sync();
     Affine<HFq2> part = xyzz_bytes_to_affine<HFq2>(C.pin_at(Ctx::kPinLvl0, 4 * sizeof(Fq2), 4 << 10));
     if (G == 1) return part;
     return sum_affine(allgather_affine(*C.comm, part));
@@ -902,15 +928,26 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
                        I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
         kp_end(I.rows_bytes, C.stream);
     }
-    // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
-    if (!o.stub) commit_launch(C, *P, z, n, G, rank);
-    // The shared level-0 opening proof is launched here, before any challenge, when the host has the
-    // matrix absorption to do meanwhile. With the index-cached transcript there is nothing to hide it
-    // behind: it then runs inside the first opening's batch (one MSM pipeline less on the critical
-    // path) and is reused by the second opening.
+    // The shared level-0 opening proof is launched right behind the commitment, before any challenge,
+    // when the host has the matrix absorption to do meanwhile. With the index-cached transcript there
+    // is nothing to hide it behind: it then runs on the context's second stream, beside the commitment
+    // and the first opening, and is reused by the second opening (SPX_LVL0_SIDE=0: inside the first
+    // opening's batch instead, one MSM pipeline less on the critical path).
     const bool share0 = !o.stub && lvl0_local(L, G);
     const bool early0 = share0 && !(o.cached && I.has_cache);
+    static const bool side_ok = [] {
+        const char* e = getenv("SPX_LVL0_SIDE");
+        return !(e && e[0] == '0');
+    }();
+    const bool side0 = share0 && !early0 && side_ok;
+    if (side0) {  // z is in place: the second stream may start
+        C.ensure_side();
+        SPX_HIP(hipEventRecord(C.side_ev, C.stream));
+    }
+    // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
+    if (!o.stub) commit_launch(C, *P, z, n, G, rank);
     if (early0) lvl0_launch(C, *P, zl, L, G, rank);
+    if (side0) lvl0_launch(C, *P, zl, L, G, rank, true);
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
@@ -955,7 +992,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, zl, L, pt1, G, rank, early0 ? &proof0 : nullptr);
+        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G)
+                            : open_z(C, *P, zl, L, pt1, G, rank, (early0 || side0) ? &proof0 : nullptr);
+        if (side0) op.proofs[0] = proof0 = lvl0_finish(C, G, true);
         if (share0 && !early0) proof0 = op.proofs[0];
         size_t m0 = proof.b.size();
         ser_open(proof, op.eval, h_of(P), op.proofs);

@@ -122,6 +122,12 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     MsmWorkspace* msm = nullptr;
+    // second stream + MSM workspace (created on first use): the shared level-0 opening MSM of an
+    // index-cached-transcript proof runs there, beside the commitment and the first opening
+    hipStream_t side = nullptr;
+    MsmWorkspace* msm_side = nullptr;
+    hipEvent_t side_ev = nullptr;
+    void ensure_side();
     std::unique_ptr<Comm> comm;
     // Pinned host staging, one fixed carve-out per context (allocated once, never moved: a region a
     // caller holds stays valid while its async copies run). Every region is reused only after a

@@ -275,6 +275,36 @@ def roofline_valu(stats, dom):
     return roof
 
 
+SETUP_KERNELS = ("k_fixed_base", "k_precompute", "k_normalize", "k_aff_to_r29", "k_to_mont", "k_points_",
+                 "__amd_rocclr_copyBufferRect")
+
+
+def whole_proof_valu(ms_per_proof):
+    """every per-proof kernel's VALU wave-instructions (committed PMC pass, one proof in flight; setup and
+    PP-preprocessing kernels excluded), issued in the measured throughput time per proof, against the chip's
+    VALU issue peak: how busy the batch keeps the vector ALUs"""
+    try:
+        ks = json.load(open(PMC_FILE))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    proofs = (ks.get("k_accum_aff<Fq >") or {}).get("launches_valu_pass")  # one commitment MSM per proof
+    if not proofs or not ms_per_proof:
+        return None
+    tot = 0.0
+    for k, v in ks.items():
+        if k.startswith(SETUP_KERNELS):
+            continue
+        vi, n = v.get("SQ_INSTS_VALU_per_launch"), v.get("launches_valu_pass")
+        if vi and n:
+            tot += vi * n
+    per = tot / proofs
+    ach = per / (ms_per_proof / 1e3)
+    return {"valu_insts_per_proof": round(per), "ms_per_proof": round(ms_per_proof, 3),
+            "achieved": round(ach / 1e9, 1), "peak": round(VALU_PEAK_WAVE_INSTR / 1e9, 1), "unit": "G VALU wave-instructions/s",
+            "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
+            "source": "profiles/pmc_kernels.json (per-proof kernels of the PMC pass, %d proofs)" % proofs}
+
+
 def madd_register_resident():
     """lane-pair G2 mixed additions per second of x29_madd on register-resident operands"""
     try:
@@ -527,6 +557,10 @@ def main():
             hb = roofline_hbm(alone)
             if hb:
                 roof["hbm_kernels"] = hb
+            if world == 1:
+                wp = whole_proof_valu(ms / P)
+                if wp:
+                    roof["whole_proof"] = wp
     cpu = cpu_all = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.kind, args.cpu_log_n if not stub else 16, log_v, args.cpu_seconds, stub=stub)

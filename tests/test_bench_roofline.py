@@ -1,0 +1,53 @@
+"""bench.py's roofline bookkeeping (host logic, no GPU): the per-launch PMC counters are scaled to the
+run's launch size, and the whole-proof VALU rate counts only per-proof kernels."""
+import importlib.util
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _pmc():
+    return json.load(open(os.path.join(ROOT, "profiles", "pmc_kernels.json")))["kernels"]
+
+
+def test_valu_roofline_scales_counters_to_the_launch(bench):
+    pm = _pmc()["k_accum_aff<Fq2>"]
+    alg = pm["alg_bytes_per_launch"]
+    full = {"msm_acc_g2": {"launches": 3.0, "ms": 3 * 4.0, "bytes": 3 * alg, "ops": 0.0}}
+    half = {"msm_acc_g2": {"launches": 3.0, "ms": 3 * 2.0, "bytes": 3 * alg / 2, "ops": 0.0}}
+    a = bench.roofline_valu(full, "msm_acc_g2")
+    b = bench.roofline_valu(half, "msm_acc_g2")
+    assert a["pmc_share"] == pytest.approx(1.0)
+    assert b["pmc_share"] == pytest.approx(0.5)
+    assert b["valu_insts_per_launch"] == pytest.approx(a["valu_insts_per_launch"] / 2)
+    # half the work in half the time: the same issue rate, the same traffic ratio
+    assert b["frac"] == pytest.approx(a["frac"], rel=1e-3)
+    assert b["hbm"]["traffic_over_algorithmic"] == pytest.approx(a["hbm"]["traffic_over_algorithmic"], rel=1e-3)
+    assert 0 < a["frac"] < 1
+
+
+def test_whole_proof_valu_excludes_setup_kernels(bench):
+    ks = _pmc()
+    wp = bench.whole_proof_valu(17.5)
+    proofs = ks["k_accum_aff<Fq >"]["launches_valu_pass"]
+    setup = sum(v["SQ_INSTS_VALU_per_launch"] * v["launches_valu_pass"] for k, v in ks.items()
+                if k.startswith(bench.SETUP_KERNELS) and v.get("SQ_INSTS_VALU_per_launch"))
+    every = sum(v["SQ_INSTS_VALU_per_launch"] * v["launches_valu_pass"] for v in ks.values()
+                if v.get("SQ_INSTS_VALU_per_launch") and v.get("launches_valu_pass"))
+    assert setup > 0
+    assert wp["valu_insts_per_proof"] == pytest.approx((every - setup) / proofs, rel=1e-6)
+    # the accumulation kernels alone are most of a proof's instructions
+    acc = sum(ks[k]["SQ_INSTS_VALU_per_launch"] * ks[k]["launches_valu_pass"] for k in ("k_accum_aff<Fq2>", "k_accum_aff<Fq >"))
+    assert acc / proofs < wp["valu_insts_per_proof"] < 1.3 * acc / proofs
+    assert 0 < wp["frac"] < 1

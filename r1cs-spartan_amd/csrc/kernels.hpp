@@ -138,21 +138,45 @@ struct MsmInst {
     uint64_t scalar_off;  // first scalar (Montgomery Fr) in the batch scalar array
     uint32_t size;        // number of (base, scalar) pairs
     uint32_t c, W;        // window bits, windows
-    uint32_t bucket_off;  // first bucket of this instance (2^(c-1) buckets)
-    uint32_t ref_off;     // first (bucket, reference) slot of this instance (radix-sort layout)
-    uint32_t stride;      // points per window copy of the base set (>= size; local blocks)
+    uint32_t stride;      // points per window copy of the base set (>= size)
+    // filled in by the MSM driver:
+    uint32_t bucket_off;  // first local bucket of this instance
+    uint32_t ref_off;     // first (bucket, reference) slot of this instance (dense key layout)
+    uint32_t lb;          // log2 of the buckets this rank weights: c - 1 (whole) or c - 1 - log2(world) (split)
+    uint32_t sel;         // this rank's bucket range [sel << lb, (sel + 1) << lb) of the 2^(c-1)
+    uint32_t out;         // output slot (index in the caller's instance list)
+    uint32_t pad;
 };
+
+// Bucket-range partition of a batch over the ranks of a proof-sharded prove: every
+// rank reads ALL scalars of an instance and keeps the digits whose bucket lies in its range, so the
+// accumulation, the partial levels and the bucket weighting all divide by the world size. Rank r's
+// result for an instance is sum_{j in its range} (j + 1) S_j; the ranks' results sum to the MSM.
+// Instances too small to split (fewer than 4 buckets per rank) go whole to rank (index mod world).
+struct MsmShard {
+    int rank = 0, world = 1;
+    bool dense = false;  // world > 1: one key slot per (scalar, window), as at world 1 (never overflows)
+};
+static constexpr uint32_t kMsmOverflow = 1;  // status bit: compacted keys exceeded their capacity
 
 struct MsmWorkspace;  // opaque, owned by the host side (msm.hip)
 MsmWorkspace* msm_ws_create();
 void msm_ws_destroy(MsmWorkspace* ws);
+// the pinned staging of the small per-batch tables: call only after a sync covering the workspace's stream
+void msm_ws_staging_reset(MsmWorkspace* ws);
+// a batch of this workspace reported kMsmOverflow: raise its compacted-key capacity for later batches
+void msm_ws_note_overflow(MsmWorkspace* ws);
 
-// Runs a batch of MSMs on `s`; out_xyzz receives one XYZZ point per instance (G1: 4 x 48 B,
-// G2: 4 x 96 B, Montgomery limbs). Synchronises once on `s` to size the accumulation levels.
+// bytes of a batch's output buffer: one XYZZ point per instance (G1: 4 x 48 B, G2: 4 x 96 B,
+// Montgomery limbs; infinity = all zero), then a 16-byte status word (kMsmOverflow)
+inline size_t msm_out_bytes(bool g2, int ninst) { return (size_t)ninst * (g2 ? 4 * 96 : 4 * 48) + 16; }
+// Enqueues a batch of MSMs on `s` without any host synchronisation. With world > 1 and !dense the
+// keys are compacted into a capacity planned from the expected bucket occupancy; if the status word
+// reads kMsmOverflow afterwards, the outputs are invalid and the batch must be rerun with dense = true.
 void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G1Slot* pts, const Fr* scalars,
-                void* out_xyzz_dev, hipStream_t s);
+                void* out_dev, hipStream_t s, const MsmShard& sh = MsmShard());
 void msm_run_g2(MsmWorkspace* ws, const MsmInst* insts_host, int ninst, const G2Aff* pts, const Fr* scalars,
-                void* out_xyzz_dev, hipStream_t s);
+                void* out_dev, hipStream_t s, const MsmShard& sh = MsmShard());
 
 // PP preprocessing: for each base B_j (raw affine, level array), write the W window copies
 // 2^(c w) B_j (affine) to dst[w * count + j]. pair_sum: B_j := raw[2j] + raw[2j+1].

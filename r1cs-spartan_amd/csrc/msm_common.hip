@@ -11,14 +11,16 @@
 //  * Signed c-bit digits -> (bucket, reference) pairs written window-major, hipCUB LSD radix sort
 //    on the bucket bits, run boundaries -> per-bucket counts and offsets. References are 32-bit
 //    point indices with the sign in bit 31. Order inside a bucket is irrelevant: group addition is
-//    exact and commutative, the affine result is unique. (SPX_MSM_SORT=atomic: the older atomic
-//    histogram + atomic scatter counting sort.)
+//    exact and commutative, the affine result is unique.
+//  * Proof-sharded ranks split every instance by BUCKET range (MsmShard, kernels.hpp): each rank
+//    digitises all scalars but keeps only its range's digits (compacted), so every stage after the
+//    digit pass divides by the world size, the bucket weighting included.
 //  * Bucket accumulation in XYZZ coordinates: the affine level gives every thread the same number
 //    of consecutive references of the sorted array across bucket boundaries (a thread crossing a
-//    boundary stores a partial and restarts), then XYZZ levels over the partials of each bucket
-//    until every bucket has one value (one host sync to read the largest bucket).
+//    boundary stores a partial and restarts), then XYZZ levels over the partials of each bucket,
+//    as many as the expected occupancy needs; the weighting leaf adds whatever partials remain.
 //  * Bucket weighting sum_j j S_j as a low-depth (F, S, D) tree (msm_impl.hpp).
-// Many MSMs run as one batch (all nv levels of an opening): one pipeline, one sync.
+// Many MSMs run as one batch (all nv levels of an opening), and nothing in it waits for the host.
 #include "msm_common.hpp"
 
 #include <algorithm>
@@ -32,81 +34,95 @@ __device__ __constant__ constexpr uint32_t kFqR2[12] = {0x1c341746u, 0xf4df1f34u
                                                        0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, 0x67eb88a9u,
                                                        0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u};
 
-// ------------------------------------------------------------------ digits: count / scatter
-template <bool SCATTER>
-__global__ __launch_bounds__(kLight) void k_msm_digits(const MsmInst* __restrict__ insts,
-                                                       const uint64_t* __restrict__ prefix, int ninst,
-                                                       uint64_t total, const Fr* __restrict__ scalars,
-                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ cursor,
-                                                       uint32_t* __restrict__ refs) {
-    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    const int i = find_slot(prefix, ninst, g);
-    const uint64_t j = g - prefix[i];
-    const MsmInst I = insts[i];
-    Fr m, s;
-    load_vec(m, scalars + I.scalar_off + j);
-    fe_from_mont(s, m);
-    const uint32_t c = I.c, full = 1u << c, half = full >> 1, mask = full - 1;
+// ------------------------------------------------------------------ digits -> (bucket, reference) keys
+// Signed c-bit digits of a canonical scalar, least significant window first.
+struct Digits {
+    uint32_t s[8];
     uint32_t carry = 0;
-    for (uint32_t w = 0; w < I.W; ++w) {
-        uint32_t v = (s.v[0] & mask) + carry;
+    DEV int32_t next(uint32_t c) {
+        const uint32_t full = 1u << c, half = full >> 1;
+        uint32_t v = (s[0] & (full - 1)) + carry;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
-        s.v[7] >>= c;
-        int32_t d;
-        if (v > half) {
-            d = (int32_t)v - (int32_t)full;
-            carry = 1;
-        } else {
-            d = (int32_t)v;
-            carry = 0;
-        }
-        if (d != 0) {
-            const uint32_t b = I.bucket_off + (uint32_t)(d < 0 ? -d : d) - 1;
-            if (!SCATTER) {
-                atomicAdd(&counts[b], 1u);
-            } else {
-                const uint32_t pos = atomicAdd(&cursor[b], 1u);
-                refs[pos] = (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
-            }
-        }
+        for (int k = 0; k < 7; ++k) s[k] = (s[k] >> c) | (s[k + 1] << (32 - c));
+        s[7] >>= c;
+        carry = v > half;
+        return carry ? (int32_t)v - (int32_t)full : (int32_t)v;
     }
+};
+// the digit's bucket if it lies in this rank's range of the instance (local index in the batch), else ~0u
+DEV uint32_t digit_key(const MsmInst& I, int32_t d) {
+    if (!d) return ~0u;
+    const uint32_t u = (uint32_t)(d < 0 ? -d : d) - 1;  // 0 .. 2^(c-1) - 1
+    if ((u >> I.lb) != I.sel) return ~0u;
+    return I.bucket_off + (u & ((1u << I.lb) - 1));
+}
+DEV uint32_t digit_ref(const MsmInst& I, uint32_t w, uint64_t j, int32_t d) {
+    return (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
 }
 
-// Radix-sort variant of the bucket sort: one pass writes a (bucket, reference) pair for every
-// (scalar, window), window-major within each instance so the stores coalesce; zero digits get the
-// key nb and sort last.
+// One thread per scalar. Dense: a (key, reference) pair for every (scalar, window), window-major
+// within each instance so the stores coalesce; digits that are zero or outside the rank's range get
+// the key nb and sort last. Compact (proof-sharded ranks): only in-range digits, appended through
+// a block-level scan and one atomic per block; pairs past `cap` are dropped and flag the status.
+template <bool COMPACT>
 __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
-                                                     int ninst, uint64_t total, uint32_t nb,
-                                                     const Fr* __restrict__ scalars, uint32_t* __restrict__ keys,
-                                                     uint32_t* __restrict__ vals) {
+                                                     int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
+                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                     uint32_t* __restrict__ cursor, uint32_t cap,
+                                                     uint32_t* __restrict__ status) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    const int i = find_slot(prefix, ninst, g);
-    const uint64_t j = g - prefix[i];
-    const MsmInst I = insts[i];
-    Fr m, s;
-    load_vec(m, scalars + I.scalar_off + j);
-    fe_from_mont(s, m);
-    const uint32_t c = I.c, full = 1u << c, half = full >> 1, mask = full - 1;
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < I.W; ++w) {
-        uint32_t v = (s.v[0] & mask) + carry;
+    const bool live = g < total;
+    if (!COMPACT && !live) return;
+    MsmInst I{};
+    uint64_t j = 0;
+    Digits d0;
+    if (live) {
+        const int i = find_slot(prefix, ninst, g);
+        j = g - prefix[i];
+        I = insts[i];
+        Fr m, s;
+        load_vec(m, scalars + I.scalar_off + j);
+        fe_from_mont(s, m);
 #pragma unroll
-        for (int k = 0; k < 7; ++k) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
-        s.v[7] >>= c;
-        int32_t d;
-        if (v > half) {
-            d = (int32_t)v - (int32_t)full;
-            carry = 1;
-        } else {
-            d = (int32_t)v;
-            carry = 0;
+        for (int k = 0; k < 8; ++k) d0.s[k] = s.v[k];
+    }
+    if constexpr (!COMPACT) {
+        for (uint32_t w = 0; w < I.W; ++w) {
+            const int32_t d = d0.next(I.c);
+            const uint32_t key = digit_key(I, d);
+            const uint64_t o = I.ref_off + (uint64_t)w * I.size + j;
+            keys[o] = key == ~0u ? nb : key;
+            vals[o] = digit_ref(I, w, j, d);
         }
-        const uint64_t o = I.ref_off + (uint64_t)w * I.size + j;
-        keys[o] = d ? I.bucket_off + (uint32_t)(d < 0 ? -d : d) - 1 : nb;
-        vals[o] = (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
+    } else {
+        uint32_t cnt = 0;
+        if (live) {
+            Digits d = d0;
+            for (uint32_t w = 0; w < I.W; ++w) cnt += digit_key(I, d.next(I.c)) != ~0u;
+        }
+        using Scan = hipcub::BlockScan<uint32_t, kLight>;
+        __shared__ typename Scan::TempStorage tmp;
+        __shared__ uint32_t base;
+        uint32_t pre, agg;
+        Scan(tmp).ExclusiveSum(cnt, pre, agg);
+        if (threadIdx.x == 0) {
+            base = agg ? atomicAdd(cursor, agg) : 0u;
+            if ((uint64_t)base + agg > cap) atomicOr(status, kMsmOverflow);
+        }
+        __syncthreads();
+        if (!cnt) return;
+        uint64_t pos = (uint64_t)base + pre;
+        Digits d = d0;
+        for (uint32_t w = 0; w < I.W; ++w) {
+            const int32_t dg = d.next(I.c);
+            const uint32_t key = digit_key(I, dg);
+            if (key == ~0u) continue;
+            if (pos < cap) {
+                keys[pos] = key;
+                vals[pos] = digit_ref(I, w, j, dg);
+            }
+            ++pos;
+        }
     }
 }
 // sorted keys -> first index and end of every bucket's run (ends pre-zeroed; starts of empty buckets unset)
@@ -124,16 +140,6 @@ __global__ void k_bucket_counts(const uint32_t* __restrict__ offs, const uint32_
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nb) cnt[b] = ends[b] ? ends[b] - offs[b] : 0;
     if (b == nb) cnt[b] = 0;
-}
-
-// Default: radix (measured at 2^20, 16 proofs in flight: 42.5 vs 39.0 M constraints/s for the
-// atomic count/scatter sort, which SPX_MSM_SORT=atomic selects).
-static bool sort_by_radix() {
-    static const bool v = [] {
-        const char* e = getenv("SPX_MSM_SORT");
-        return !(e && std::string(e) == "atomic");
-    }();
-    return v;
 }
 
 __global__ void k_seg_counts(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t* __restrict__ segcnt,
@@ -201,6 +207,12 @@ uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_pe
 
 MsmWorkspace* msm_ws_create() { return new MsmWorkspace(); }
 void msm_ws_destroy(MsmWorkspace* ws) { delete ws; }
+void msm_ws_staging_reset(MsmWorkspace* ws) {
+    if (ws) ws->pin.reset();
+}
+void msm_ws_note_overflow(MsmWorkspace* ws) {
+    if (ws) ws->cap_scale = std::min(ws->cap_scale * 1.5, 64.0);
+}
 
 void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
     size_t tb = 0;
@@ -209,30 +221,71 @@ void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
 }
 
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s) {
+static double msm_cap_env() {  // SPX_MSM_CAP_SCALE (tests): scales the compacted-key capacity, e.g. 0.5 forces overflow
+    const char* e = getenv("SPX_MSM_CAP_SCALE");
+    const double v = e ? atof(e) : 1.0;
+    return v > 0 ? v : 1.0;
+}
+
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s,
+                   const MsmShard& sh, uint32_t* status) {
     MsmSorted o;
-    o.insts.assign(ih, ih + ninst);
-    std::vector<uint64_t> prefix(ninst + 1);
+    const int G = std::max(1, sh.world);
+    int g = 0;
+    while ((1 << g) < G) ++g;
+    if ((1 << g) != G || sh.rank < 0 || sh.rank >= G) throw std::runtime_error("MSM shard: bad rank / world");
+    const bool compact = G > 1 && !sh.dense;
+    std::vector<uint64_t> prefix;
     uint64_t tot_sc = 0, tot_refs = 0;
+    double split_refs = 0, whole_refs = 0;
+    int nsplit = 0;
     uint32_t nb = 0;
     for (int i = 0; i < ninst; ++i) {
-        MsmInst& I = o.insts[i];
+        MsmInst I = ih[i];
+        if (!I.size || I.c < 3 || I.c > 24) {
+            if (!I.size) continue;  // empty MSM: infinity
+            throw std::runtime_error("MSM window bits out of range");
+        }
+        const uint32_t lbf = I.c - 1;  // log2 of the instance's buckets
+        if (G > 1 && (int)lbf - g >= 2) {  // split by bucket range
+            I.lb = lbf - g;
+            I.sel = (uint32_t)sh.rank;
+            split_refs += (double)I.size * I.W / G;
+            ++nsplit;
+        } else if (i % G == sh.rank) {  // whole, on its owner
+            I.lb = lbf;
+            I.sel = 0;
+            whole_refs += (double)I.size * I.W;
+        } else {
+            continue;
+        }
+        I.out = (uint32_t)i;
         I.bucket_off = nb;
         I.ref_off = (uint32_t)tot_refs;
-        nb += 1u << (I.c - 1);
-        prefix[i] = tot_sc;
+        nb += 1u << I.lb;
+        prefix.push_back(tot_sc);
         tot_sc += I.size;
         tot_refs += (uint64_t)I.size * I.W;
+        o.mu_max = std::max(o.mu_max, (double)I.size * I.W / (double)(1u << lbf));
+        o.any_sel |= I.sel != 0;
+        o.insts.push_back(I);
     }
-    prefix[ninst] = tot_sc;
+    const int nact = (int)o.insts.size();
+    prefix.push_back(tot_sc);
     if (tot_refs >= 0xffffffffull) throw std::runtime_error("MSM batch too large");
+    if (compact) {
+        // expected in-range digits plus a margin: ~8 standard deviations of the uniform case and a fixed
+        // slack per instance (the top window of a small-c instance crowds the low buckets)
+        const double cap = whole_refs + (split_refs + 8.0 * std::sqrt(split_refs) + 2048.0 * nsplit) * ws->cap_scale * msm_cap_env();
+        tot_refs = std::min<uint64_t>(tot_refs, (uint64_t)std::ceil(cap));
+    }
     o.nb = nb;
     o.tot_refs = tot_refs;
-    o.d_insts = (MsmInst*)ws->insts.ensure(sizeof(MsmInst) * ninst);
-    auto* d_prefix = (uint64_t*)ws->prefix.ensure(8 * (ninst + 1));
-    HIPCHK(hipMemcpyAsync(o.d_insts, ws->pin.stage(o.insts.data(), ninst), sizeof(MsmInst) * ninst,
-                          hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_prefix, ws->pin.stage(prefix.data(), ninst + 1), 8 * (ninst + 1), hipMemcpyHostToDevice, s));
+    if (!nact) return o;
+    o.d_insts = (MsmInst*)ws->insts.ensure(sizeof(MsmInst) * nact);
+    auto* d_prefix = (uint64_t*)ws->prefix.ensure(8 * (nact + 1));
+    HIPCHK(hipMemcpyAsync(o.d_insts, ws->pin.stage(o.insts.data(), nact), sizeof(MsmInst) * nact, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_prefix, ws->pin.stage(prefix.data(), nact + 1), 8 * (nact + 1), hipMemcpyHostToDevice, s));
     o.counts = (uint32_t*)ws->counts.ensure(4 * (nb + 1));
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
     uint32_t* cursor = (uint32_t*)ws->cursor.ensure(4 * (nb + 1));
@@ -241,57 +294,38 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* sca
     o.soa = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
     o.sob = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
     o.spare = cursor;
-    auto* d_max = (uint32_t*)ws->maxv.ensure(4);
-    if (tot_sc && sort_by_radix()) {
-        // (bucket, reference) pairs, LSD radix sort on the bucket bits, runs -> offsets and counts
-        const uint64_t n = tot_refs;
-        int bits = 1;
-        while ((1ull << bits) <= nb) ++bits;  // keys are 0..nb
-        uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * n);
-        uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * n);
-        uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * n);
-        const int gsc = (int)((tot_sc + kLight - 1) / kLight);
-        kp_begin(KP_SORT, s);
-        hipLaunchKernelGGL(k_msm_keys, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, ninst, tot_sc, nb, scalars, ka,
-                           va);
-        hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
-        size_t tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
-        void* t = ws->cub.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
-        o.refs = dv.Current();
-        HIPCHK(hipMemsetAsync(cursor, 0, 4 * (nb + 1), s));
-        hipLaunchKernelGGL(k_bucket_runs, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, dk.Current(), n,
-                           nb, o.offs, cursor);
-        hipLaunchKernelGGL(k_bucket_counts, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, o.offs, cursor, nb,
-                           o.counts);
-        exclusive_scan(ws, o.counts, o.offs, nb + 1, s);  // = run starts; empty buckets share the next offset
-        kp_end(32.0 * tot_sc + 4.0 * 8 * n, s);
-    } else if (tot_sc) {
-        HIPCHK(hipMemsetAsync(o.counts, 0, 4 * (nb + 1), s));
-        const int gsc = (int)((tot_sc + kLight - 1) / kLight);
-        kp_begin(KP_SORT, s);
-        hipLaunchKernelGGL(k_msm_digits<false>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, ninst, tot_sc,
-                           scalars, o.counts, nullptr, nullptr);
-        kp_end(32.0 * tot_sc, s);
-        exclusive_scan(ws, o.counts, o.offs, nb + 1, s);
-        HIPCHK(hipMemcpyAsync(cursor, o.offs, 4 * (nb + 1), hipMemcpyDeviceToDevice, s));
-        kp_begin(KP_SORT, s);
-        hipLaunchKernelGGL(k_msm_digits<true>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, ninst, tot_sc,
-                           scalars, nullptr, cursor, o.refs);
-        kp_end(32.0 * tot_sc + 4.0 * tot_refs, s);
+    // (bucket, reference) pairs, LSD radix sort on the bucket bits, runs -> offsets and counts
+    const uint64_t n = tot_refs;
+    int bits = 1;
+    while ((1ull << bits) <= nb) ++bits;  // keys 0..nb; the compact filler ~0 has all these bits set
+    uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * std::max<uint64_t>(n, 1));
+    uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * std::max<uint64_t>(n, 1));
+    uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
+    const int gsc = (int)((tot_sc + kLight - 1) / kLight);
+    kp_begin(KP_SORT, s);
+    if (compact) {
+        uint32_t* kc = (uint32_t*)ws->kcur.ensure(4);
+        HIPCHK(hipMemsetAsync(kc, 0, 4, s));
+        HIPCHK(hipMemsetAsync(ka, 0xff, 4 * n, s));
+        hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, nact, tot_sc, nb, scalars,
+                           ka, va, kc, (uint32_t)n, status);
     } else {
-        HIPCHK(hipMemsetAsync(o.counts, 0, 4 * (nb + 1), s));
-        exclusive_scan(ws, o.counts, o.offs, nb + 1, s);
+        hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, nact, tot_sc, nb, scalars,
+                           ka, va, nullptr, 0u, nullptr);
     }
+    hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
     size_t tb = 0;
-    HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, o.counts, d_max, nb, s));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
     void* t = ws->cub.ensure(tb);
-    HIPCHK(hipcub::DeviceReduce::Max(t, tb, o.counts, d_max, nb, s));
-    HIPCHK(hipMemcpyAsync(ws->h_max, d_max, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    ws->pin.reset();  // every copy staged so far (this batch's and the previous batch's tree tables) is done
-    o.maxc = *ws->h_max;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
+    o.refs = dv.Current();
+    HIPCHK(hipMemsetAsync(cursor, 0, 4 * (nb + 1), s));
+    hipLaunchKernelGGL(k_bucket_runs, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, dk.Current(), n, nb,
+                       o.offs, cursor);
+    hipLaunchKernelGGL(k_bucket_counts, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, o.offs, cursor, nb,
+                       o.counts);
+    exclusive_scan(ws, o.counts, o.offs, nb + 1, s);  // = run starts; empty buckets share the next offset
+    kp_end(32.0 * tot_sc + 4.0 * 8 * n, s);
     return o;
 }
 

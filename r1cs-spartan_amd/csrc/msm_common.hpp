@@ -89,10 +89,11 @@ struct DBuf {
 // Pinned host staging for the small per-batch tables an MSM uploads (instance descriptors, scalar
 // prefixes, weighting-tree prefixes). A hipMemcpyAsync from pageable memory may read its source
 // after the call returns, so the source must outlive the copy: regions are bump-allocated and the
-// arena is reset only right after a stream synchronisation that covers every copy issued from it
-// (msm_sort's). Fixed capacity: nothing is ever reallocated under an in-flight copy.
+// arena is reset only by the workspace's owner, right after a stream synchronisation that covers
+// every copy issued from it (msm_ws_staging_reset). Fixed capacity: nothing is ever reallocated
+// under an in-flight copy.
 struct PinArena {
-    static constexpr size_t kCap = 256 << 10;
+    static constexpr size_t kCap = 512 << 10;
     uint8_t* p = nullptr;
     size_t used = 0;
     PinArena() { HIPCHK(hipHostMalloc((void**)&p, kCap)); }
@@ -111,28 +112,29 @@ struct PinArena {
 };
 
 struct MsmWorkspace {
-    DBuf insts, prefix, redp, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, maxv,
-        tprefix, keys_a, keys_b, vals_a;
-    uint32_t* h_max = nullptr;
+    DBuf insts, prefix, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, tprefix,
+        keys_a, keys_b, vals_a, kcur;
+    // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
+    // bucket ranges (e.g. many equal values) stops overflowing after its first batch
+    double cap_scale = 1.0;
     PinArena pin;
-    MsmWorkspace() { HIPCHK(hipHostMalloc((void**)&h_max, sizeof(uint32_t))); }
-    ~MsmWorkspace() {
-        if (h_max) (void)hipHostFree(h_max);
-    }
 };
 
 void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
 
-// Result of the digit / counting-sort stage of a batch (device pointers into the workspace).
+// Result of the digit / sort stage of a batch (device pointers into the workspace).
 struct MsmSorted {
-    uint32_t nb = 0;          // buckets in the batch
-    uint64_t tot_refs = 0;    // (scalar, window) references with a non-zero digit (upper bound: size * W)
-    uint32_t maxc = 0;        // largest bucket
+    uint32_t nb = 0;          // local buckets in the batch (this rank's ranges)
+    uint64_t tot_refs = 0;    // key slots: upper bound of the (scalar, window) references with a digit in range
+    double mu_max = 0;        // largest expected references per bucket over the batch's instances
+    bool any_sel = false;     // some instance weights a bucket range that does not start at bucket 0
     uint32_t *counts, *offs, *refs, *segcnt, *soa, *sob, *spare;
     MsmInst* d_insts;
-    std::vector<MsmInst> insts;  // host copy with bucket offsets filled in
+    std::vector<MsmInst> insts;  // host copy of the active instances, driver fields filled in
 };
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s);
+// instances of `ih` this rank works on, keys of their in-range digits sorted by bucket
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s,
+                   const MsmShard& sh, uint32_t* status);
 // partials of the load-balanced affine level per bucket: the seg-length thread ranges its references meet
 void launch_partial_counts(const uint32_t* off, const uint32_t* cnt, uint32_t nb, uint32_t* np, uint32_t seg,
                            hipStream_t s);

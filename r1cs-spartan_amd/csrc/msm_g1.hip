@@ -9,8 +9,8 @@
 namespace spx {
 
 void msm_run_g1(MsmWorkspace* ws, const MsmInst* insts, int ninst, const G1Slot* pts, const Fr* scalars, void* out,
-                hipStream_t s) {
-    msm_run_t<Fq>(ws, insts, ninst, pts, scalars, out, s);
+                hipStream_t s, const MsmShard& sh) {
+    msm_run_t<Fq>(ws, insts, ninst, pts, scalars, out, s, sh);
 }
 void precompute_windows_g1(const G1Aff* raw, uint64_t count, bool pair_sum, int c, int W, G1Aff* dst, void* tmp,
                            hipStream_t s) {

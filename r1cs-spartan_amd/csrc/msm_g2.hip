@@ -10,8 +10,8 @@
 namespace spx {
 
 void msm_run_g2(MsmWorkspace* ws, const MsmInst* insts, int ninst, const G2Aff* pts, const Fr* scalars, void* out,
-                hipStream_t s) {
-    msm_run_t<Fq2>(ws, insts, ninst, pts, scalars, out, s);
+                hipStream_t s, const MsmShard& sh) {
+    msm_run_t<Fq2>(ws, insts, ninst, pts, scalars, out, s, sh);
 }
 void precompute_windows_g2(const G2Aff* raw, uint64_t count, bool pair_sum, int c, int W, G2Aff* dst, void* tmp,
                            hipStream_t s) {

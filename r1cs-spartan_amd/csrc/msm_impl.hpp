@@ -371,8 +371,11 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uin
 // depth per level (single-lane latency of a G2 addition is ~45 us on CDNA4).
 // A missing right child (instances with fewer chunks) is the point at infinity: F and S pass
 // through unchanged, so all instances of a batch run the same number of levels.
-DEV uint32_t tree_chunk_log(uint32_t c) { return c - 2 < kTreeChunkLog ? c - 2 : kTreeChunkLog; }
+// lb = log2 of the instance's (local) buckets >= 1; chunks of 2^lgm buckets, lgm <= lb - 1
+DEV uint32_t tree_chunk_log(uint32_t lb) { return lb - 1 < kTreeChunkLog ? lb - 1 : kTreeChunkLog; }
 
+// Every partial a bucket still has is added here (the partial levels are planned from the expected
+// occupancy, so a crowded bucket may arrive with several): run += X for each, then F += run.
 template <class F>
 __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp, int ninst, const uint32_t* __restrict__ node_off,
@@ -384,29 +387,33 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     const int i = find_slot(wp, ninst, t);
     const uint32_t k = (uint32_t)(t - wp[i]);
     const MsmInst I = insts[i];
-    const uint32_t lgm = tree_chunk_log(I.c);
+    const uint32_t lgm = tree_chunk_log(I.lb);
     const uint32_t b0 = I.bucket_off + (k << lgm);
     const uint32_t o = node_off[i] + k;
-    // F accumulates in its output slot, and both kinds of step (run += X_j, F += run) go through one
+    // F accumulates in its output slot, and both kinds of step (run += X, F += run) go through one
     // addition site with two points live: a G2 XYZZ point is 112 registers in radix 2^29
     using T = typename A::T;
     X29<T> run;
     x29_set_inf(run);
     const int m = 1 << lgm;
+    int j = m - 1;
+    uint32_t u = 0, nu = cnt[b0 + j];  // partials of bucket j added so far / to add
 #pragma unroll 1
-    for (int st = 0; st < 2 * m; ++st) {
-        const int j = m - 1 - (st >> 1);
-        const bool bucket_step = (st & 1) == 0;
+    for (;;) {
+        const bool bucket_step = u < nu;
         X29<T> a, b;
         if (bucket_step) {
-            if (!cnt[b0 + j]) continue;
             a = run;
-            A::ld(b, P + off[b0 + j]);
+            A::ld(b, P + off[b0 + j] + u);
+            ++u;
+        } else if (j == m - 1) {  // F = run for the top bucket
+            A::st(Fo + o, run);
+            if (j == 0) break;
+            --j;
+            u = 0;
+            nu = cnt[b0 + j];
+            continue;
         } else {
-            if (j == m - 1) {  // F = run for the top bucket
-                A::st(Fo + o, run);
-                continue;
-            }
             A::ld(a, Fo + o);
             b = run;
         }
@@ -415,7 +422,10 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
             run = a;
         } else {
             A::st(Fo + o, a);
-            run = b;
+            if (j == 0) break;
+            --j;
+            u = 0;
+            nu = cnt[b0 + j];
         }
     }
     A::st(So + o, run);
@@ -458,18 +468,44 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
         A::st(So + base + k, a);
     } else {
         A::ld(a, Di + base + 2 * k);
-        if (has_r) {
+        if (has_r) {  // a lone root passes through: D stays (its buckets) x S for k_tree_offset
             A::ld(b, Di + base + 2 * k + 1);
             tree_add<F>(a, b);
+            tree_dbl<F>(a);
         }
-        tree_dbl<F>(a);
         A::st(Do + base + k, a);
     }
 }
 
+// A rank weighting bucket range sel (buckets [sel 2^lb, (sel + 1) 2^lb) of the instance) computed
+// sum_m (m + 1) X_m over local indices; the global weights add sel 2^lb S = sel D (D of the root).
 template <class F>
-__global__ void k_tree_out(int ninst, const uint32_t* __restrict__ node_off, const Xyzz<F>* __restrict__ Fi,
-                           Xyzz<F>* __restrict__ out) {
+__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_offset(const MsmInst* __restrict__ insts, int ninst,
+                                                                        const uint32_t* __restrict__ node_off,
+                                                                        Xyzz<F>* __restrict__ Fi,
+                                                                        const Xyzz<F>* __restrict__ Di) {
+    using A = Acc<F>;
+    const uint64_t t = tree_elem<F>();
+    if (t >= (uint64_t)ninst) return;
+    const uint32_t sel = insts[t].sel;
+    if (!sel) return;
+    const uint32_t o = node_off[t];
+    X29<typename A::T> d, acc, f;
+    A::ld(d, Di + o);
+    acc = d;
+#pragma unroll 1
+    for (int b = 30 - __clz(sel); b >= 0; --b) {  // sel d, double-and-add below the top bit
+        tree_dbl<F>(acc);
+        if ((sel >> b) & 1u) tree_add<F>(acc, d);
+    }
+    A::ld(f, Fi + o);
+    tree_add<F>(f, acc);
+    A::st(Fi + o, f);
+}
+
+template <class F>
+__global__ void k_tree_out(const MsmInst* __restrict__ insts, int ninst, const uint32_t* __restrict__ node_off,
+                           const Xyzz<F>* __restrict__ Fi, Xyzz<F>* __restrict__ out) {
     using T = typename R29<F>::T;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < ninst) {  // back to the R = 2^384 Montgomery domain, canonical, for the host
@@ -479,20 +515,25 @@ __global__ void k_tree_out(int ninst, const uint32_t* __restrict__ node_off, con
         f29_map(b.y, a.y, Q29::TO_R1);
         f29_map(b.zz, a.zz, Q29::TO_R1);
         f29_map(b.zzz, a.zzz, Q29::TO_R1);
-        st29<F>(out + i, b);
+        st29<F>(out + insts[i].out, b);
     }
 }
 
 template <class F>
 static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const typename Acc<F>::Pt* pts, const Fr* scalars,
-                      void* out_dev, hipStream_t s) {
+                      void* out_dev, hipStream_t s, const MsmShard& sh) {
     if (ninst <= 0) return;
-    MsmSorted so = msm_sort(ws, ih, ninst, scalars, s);
     const bool g2 = sizeof(F) == sizeof(Fq2);
+    const size_t psz = sizeof(Xyzz<F>);
+    // every output starts at infinity (all zero) and the status word at 0
+    HIPCHK(hipMemsetAsync(out_dev, 0, msm_out_bytes(g2, ninst), s));
+    uint32_t* status = (uint32_t*)((uint8_t*)out_dev + psz * ninst);
+    MsmSorted so = msm_sort(ws, ih, ninst, scalars, s, sh, status);
+    const int nact = (int)so.insts.size();
+    if (!nact) return;
     const uint32_t nb = so.nb;
     const uint64_t tot_refs = so.tot_refs;
-    // level 1: affine references -> XYZZ partials, one per segment of kSeg references
-    const size_t psz = sizeof(Xyzz<F>);
+    // level 1: affine references -> XYZZ partials, one per segment of kSeg1 references
     const uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
@@ -513,7 +554,11 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     Xyzz<F>* cur = PA;
     Xyzz<F>* nxt = PB;
     uint64_t cur_max_segs = max_segs;
-    uint32_t m = so.maxc ? (so.maxc + kSeg1 - 1) / kSeg1 + 1 : 1;  // partials per bucket (a range may straddle)
+    // XYZZ partial levels, planned from the expected occupancy (no host round trip): a bucket with
+    // mu references on average rarely exceeds mu + 6 sqrt(mu) + 16; the weighting leaf adds the
+    // partials of any bucket that does (k_tree_chunk), so the plan decides speed, never correctness
+    const double mu = so.mu_max;
+    uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1;  // partials per bucket
     while (m > 1) {
         launch_seg_counts(cur_cnt, nb, spare_cnt, kSeg, s);
         exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
@@ -528,31 +573,31 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
         cur_max_segs = nsegs;
         m = (m + kSeg - 1) / kSeg;
     }
-    // bucket weighting tree
-    std::vector<uint32_t> node_off(ninst), cnt(ninst);
+    // bucket weighting tree over each instance's 2^lb local buckets
+    std::vector<uint32_t> node_off(nact), cnt(nact);
     uint32_t tot_nodes = 0;
     int levels = 0;
-    for (int i = 0; i < ninst; ++i) {
+    for (int i = 0; i < nact; ++i) {
         node_off[i] = tot_nodes;
-        // nodes after the chunked leaf level: B / 2^lgm (c >= 3, lgm = min(kTreeChunkLog, c - 2))
-        const int lg = (int)so.insts[i].c - 1 - (int)std::min<uint32_t>(kTreeChunkLog, so.insts[i].c - 2);
+        // nodes after the chunked leaf level: 2^lb / 2^lgm (lb >= 2, lgm = min(kTreeChunkLog, lb - 1))
+        const int lg = (int)so.insts[i].lb - (int)std::min<uint32_t>(kTreeChunkLog, so.insts[i].lb - 1);
         cnt[i] = 1u << lg;
         tot_nodes += cnt[i];
         levels = std::max(levels, lg);
     }
     // per-level work prefixes: 3 threads per output node; per-level input node counts
-    std::vector<uint64_t> wp((size_t)(levels + 1) * (ninst + 1));
-    std::vector<uint32_t> cin((size_t)(levels + 1) * ninst);
+    std::vector<uint64_t> wp((size_t)(levels + 1) * (nact + 1));
+    std::vector<uint32_t> cin((size_t)(levels + 1) * nact);
     for (int lv = 0; lv <= levels; ++lv) {
         uint64_t acc = 0;
-        for (int i = 0; i < ninst; ++i) {
+        for (int i = 0; i < nact; ++i) {
             uint32_t nin = lv == 0 ? (cnt[i] * 2) : std::max(1u, cnt[i] >> (lv - 1));
             uint32_t nout = lv == 0 ? cnt[i] : std::max(1u, cnt[i] >> lv);
-            cin[(size_t)lv * ninst + i] = nin;
-            wp[(size_t)lv * (ninst + 1) + i] = acc;
+            cin[(size_t)lv * nact + i] = nin;
+            wp[(size_t)lv * (nact + 1) + i] = acc;
             acc += nout;
         }
-        wp[(size_t)lv * (ninst + 1) + ninst] = acc;
+        wp[(size_t)lv * (nact + 1) + nact] = acc;
     }
     const size_t tbytes = 8 * wp.size() + 4 * cin.size() + 4 * node_off.size();
     auto* tp = (uint8_t*)ws->tprefix.ensure(tbytes);
@@ -570,17 +615,21 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     Xyzz<F>* B3[3] = {TB, TB + tot_nodes, TB + 2 * (size_t)tot_nodes};
     kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     {
-        uint64_t work = wp[ninst];
-        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, ninst, d_noff,
+        uint64_t work = wp[nact];
+        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, nact, d_noff,
                            cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
     }
     for (int lv = 1; lv <= levels; ++lv) {
-        uint64_t work = 3 * wp[(size_t)lv * (ninst + 1) + ninst];
-        hipLaunchKernelGGL(k_tree_level<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (ninst + 1),
-                           ninst, d_noff, d_cin + (size_t)lv * ninst, A3[0], A3[1], A3[2], B3[0], B3[1], B3[2]);
+        uint64_t work = 3 * wp[(size_t)lv * (nact + 1) + nact];
+        hipLaunchKernelGGL(k_tree_level<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (nact + 1),
+                           nact, d_noff, d_cin + (size_t)lv * nact, A3[0], A3[1], A3[2], B3[0], B3[1], B3[2]);
         std::swap(A3, B3);
     }
-    hipLaunchKernelGGL(k_tree_out<F>, dim3((ninst + 63) / 64), dim3(64), 0, s, ninst, d_noff, A3[0], (Xyzz<F>*)out_dev);
+    if (so.any_sel)
+        hipLaunchKernelGGL(k_tree_offset<F>, dim3(tree_blocks<F>((uint64_t)nact)), dim3(kHeavy), 0, s, so.d_insts, nact,
+                           d_noff, A3[0], A3[2]);
+    hipLaunchKernelGGL(k_tree_out<F>, dim3((nact + 63) / 64), dim3(64), 0, s, so.d_insts, nact, d_noff, A3[0],
+                       (Xyzz<F>*)out_dev);
     kp_end((double)nb * psz, s);
     HIPCHK(hipGetLastError());
 }

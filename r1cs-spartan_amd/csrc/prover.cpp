@@ -3,9 +3,12 @@
 // HIP kernels (mle_kernels.hip, msm.hip) and the Fiat-Shamir transcript on the host.
 //
 // Sharding: G = 2^g ranks own contiguous blocks of the hypercube (top g bits of x
-// or y). Variables bind LSB first, so every rank folds locally for the first L - g rounds; each
-// round exchanges 3 Fr per rank, each MSM one affine point per rank. The last g rounds/levels run on
-// the gathered G-entry tables. Every rank replays the same transcript, so no challenge broadcast.
+// or y) for the SpMV, eval_on_x and both sumchecks. Variables bind LSB first, so every rank folds
+// locally for the first L - g rounds; each round exchanges 3 Fr per rank, and the last g rounds run
+// on the gathered G-entry tables. The MSMs (commitment, openings) split every instance by bucket
+// range instead (MsmShard, kernels.hpp): z is replicated, every rank folds the opening tables in
+// full (HBM-streaming) and weights 1/G of the buckets; each MSM exchanges one XYZZ point per rank.
+// Every rank replays the same transcript, so no challenge broadcast.
 #include "prover.hpp"
 #include "pairing.hpp"
 
@@ -585,30 +588,66 @@ struct Timer {
     }
 };
 
+// device MSM output (XYZZ, R = 2^384 Montgomery limbs) -> host Jacobian without an inversion:
+// Z = ZZ ZZZ, X = x Z^2 = X ZZ ZZZ^2, Y = y Z^3 = Y ZZ^3 ZZZ^2 (ZZ = 0: infinity)
 template <class F>
-static Affine<F> xyzz_bytes_to_affine(const uint8_t* p) {
+static host::Jac<F> xyzz_bytes_to_jac(const uint8_t* p) {
     F X, Y, ZZ, ZZZ;
     memcpy(&X, p, sizeof(F));
     memcpy(&Y, p + sizeof(F), sizeof(F));
     memcpy(&ZZ, p + 2 * sizeof(F), sizeof(F));
     memcpy(&ZZZ, p + 3 * sizeof(F), sizeof(F));
-    return host::xyzz_to_affine(X, Y, ZZ, ZZZ);
+    if (ZZ.is_zero()) return host::jac_inf<F>();
+    const F z3s = ZZZ * ZZZ;
+    return {X * ZZ * z3s, Y * (ZZ * ZZ * ZZ) * z3s, ZZ * ZZZ};
+}
+template <class F>
+static std::vector<Affine<F>> jac_to_affine_batch(const std::vector<host::Jac<F>>& v) {
+    std::vector<F> zi(v.size());
+    for (size_t k = 0; k < v.size(); ++k) zi[k] = v[k].z;
+    host::batch_inverse(zi);
+    std::vector<Affine<F>> out(v.size());
+    for (size_t k = 0; k < v.size(); ++k) {
+        if (v[k].z.is_zero()) {
+            out[k] = {F::zero(), F::one(), true};
+            continue;
+        }
+        const F z2 = zi[k] * zi[k];
+        out[k] = {v[k].x * z2, v[k].y * z2 * zi[k], false};
+    }
+    return out;
 }
 
-// sum of affine points gathered from every rank
+// Outputs of an MSM batch (`cnt` instances, this rank's bucket ranges) -> the affine MSM results:
+// every rank's partial of every instance, gathered over the communicator and summed.
 template <class F>
-static Affine<F> sum_affine(const std::vector<Affine<F>>& pts) {
-    host::Jac<F> acc = host::jac_inf<F>();
-    for (auto& p : pts) acc = host::jac_add(acc, host::jac_from(p));
-    return host::jac_to_affine(acc);
-}
-
-template <class F>
-static std::vector<Affine<F>> allgather_affine(Comm& comm, const Affine<F>& mine) {
+static std::vector<Affine<F>> msm_results(Comm& comm, const uint8_t* xyzz, int cnt) {
+    const size_t psz = 4 * sizeof(F);
     const int G = comm.size();
-    std::vector<Affine<F>> all(G);
-    comm.allgather(&mine, all.data(), sizeof(Affine<F>));
-    return all;
+    std::vector<uint8_t> all;
+    const uint8_t* src = xyzz;
+    if (G > 1) {
+        all.resize(psz * cnt * G);
+        comm.allgather(xyzz, all.data(), psz * cnt);
+        src = all.data();
+    }
+    std::vector<host::Jac<F>> sum(cnt, host::jac_inf<F>());
+    for (int r = 0; r < G; ++r)
+        for (int k = 0; k < cnt; ++k) sum[k] = host::jac_add(sum[k], xyzz_bytes_to_jac<F>(src + psz * ((size_t)r * cnt + k)));
+    return jac_to_affine_batch(sum);
+}
+
+static uint32_t msm_status(const uint8_t* h, bool g2, int cnt) {
+    uint32_t st;
+    memcpy(&st, h + msm_out_bytes(g2, cnt) - 16, 4);
+    return st;
+}
+
+static MsmShard shard_of(const Comm& comm) {
+    MsmShard sh;
+    sh.rank = comm.rank();
+    sh.world = comm.size();
+    return sh;
 }
 
 static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
@@ -621,29 +660,31 @@ static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
 // ---------------------------------------------------------------- commit (commit.rs:17-29)
 // Split in two so the MSM runs while the host absorbs the matrices into the transcript: launch
 // enqueues the MSM and the copy of its XYZZ result into pinned memory; finish waits and decodes.
-static void commit_launch(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
-    const uint64_t nl = n / G, lo = (uint64_t)rank * nl;
+// Proof-sharded (world > 1): every rank holds all of z and weights its range of the buckets.
+static void commit_launch(Ctx& C, PP& P, const Fr* z, uint64_t n, const MsmShard& sh) {
     MsmInst inst{};
-    inst.pts_off = lo;
+    inst.pts_off = 0;
     inst.stride = (uint32_t)n;
-    inst.scalar_off = lo;
-    inst.size = (uint32_t)nl;
+    inst.scalar_off = 0;
+    inst.size = (uint32_t)n;
     inst.c = (uint32_t)P.g1_c;
     inst.W = (uint32_t)P.g1_W;
-    void* out = C.buf(Ctx::kSlotCommit, 4 * sizeof(Fq));
-    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Slot>(), z_full, out, C.stream);
-    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, 4 * sizeof(Fq), 4 << 10), out, 4 * sizeof(Fq),
-                           hipMemcpyDeviceToHost, C.stream));
+    const size_t ob = msm_out_bytes(false, 1);
+    void* out = C.buf(Ctx::kSlotCommit, ob);
+    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, C.stream, sh);
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, C.stream));
 }
-static Affine<HFq> commit_finish(Ctx& C, int G) {
+static Affine<HFq> commit_finish(Ctx& C, PP& P, const Fr* z, uint64_t n, Comm& comm) {
     C.sync();
-    Affine<HFq> part = xyzz_bytes_to_affine<HFq>(C.pin_at(Ctx::kPinCommit, 4 * sizeof(Fq), 4 << 10));
-    if (G == 1) return part;
-    return sum_affine(allgather_affine(*C.comm, part));
-}
-static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, int rank) {
-    commit_launch(C, P, z_full, n, G, rank);
-    return commit_finish(C, G);
+    const uint8_t* h = C.pin_at(Ctx::kPinCommit, msm_out_bytes(false, 1), 4 << 10);
+    if (msm_status(h, false, 1) & kMsmOverflow) {  // compacted keys overflowed: once more with a slot per digit
+        msm_ws_note_overflow(C.msm);
+        MsmShard sh = shard_of(comm);
+        sh.dense = true;
+        commit_launch(C, P, z, n, sh);
+        C.sync();
+    }
+    return msm_results<HFq>(comm, h, 1)[0];
 }
 
 // ---------------------------------------------------------------- level 0 of both openings
@@ -652,11 +693,10 @@ static Affine<HFq> commit_z(Ctx& C, PP& P, const Fr* z_full, uint64_t n, int G, 
 // (r_v, 0..0) (prover.rs:152) and in the one at r_y (prover.rs:275). It is computed once per proof,
 // launched right behind the commitment (before any challenge exists, overlapping the host's
 // absorption of the matrices) and handed to both open_z calls: a quarter of the proof's G2 work.
-static bool lvl0_local(int L, int G) { return L - ilog2((uint64_t)G) >= 1; }
 // on_side: on the context's second stream (ordered after the main stream's work so far), without
 // kernel statistics (they time the main stream only)
-static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank, bool on_side = false) {
-    const uint64_t half = ((1ull << L) / G) / 2;
+static void lvl0_launch(Ctx& C, PP& P, const Fr* z, int L, const MsmShard& sh, bool on_side = false) {
+    const uint64_t half = (1ull << L) / 2;
     hipStream_t st = C.stream;
     MsmWorkspace* ws = C.msm;
     struct KpRestore {
@@ -670,27 +710,36 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z_local, int L, int G, int rank
         g_kprof = nullptr;
     }
     Fr* q = C.buf<Fr>(Ctx::kSlotLvl0Q, 32 * half);
-    launch_open_level(z_local, nullptr, q, nullptr, half, st);
+    launch_open_level(z, nullptr, q, nullptr, half, st);
     MsmInst I{};
-    I.pts_off = P.g2_off[0] + (uint64_t)rank * half;
-    I.stride = (uint32_t)(1ull << (L - 1));
+    I.pts_off = P.g2_off[0];
+    I.stride = (uint32_t)half;
     I.scalar_off = 0;
     I.size = (uint32_t)half;
     I.c = (uint32_t)P.g2_c[0];
     I.W = (uint32_t)P.g2_W[0];
-    const size_t xb = 4 * sizeof(Fq2);
-    void* out = C.buf(Ctx::kSlotLvl0Out, xb);
-    msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st);
-    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, xb, 4 << 10), out, xb, hipMemcpyDeviceToHost, st));
+    const size_t ob = msm_out_bytes(true, 1);
+    void* out = C.buf(Ctx::kSlotLvl0Out, ob);
+    msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
 }
-static Affine<HFq2> lvl0_finish(Ctx& C, int G, bool on_side = false) {
+static Affine<HFq2> lvl0_finish(Ctx& C, PP& P, const Fr* z, int L, Comm& comm, bool on_side = false) {
     if (on_side)
-        SPX_HIP(hipStreamSynchronize(C.side));
+        C.side_sync();
     else
         C.sync();
-    Affine<HFq2> part = xyzz_bytes_to_affine<HFq2>(C.pin_at(Ctx::kPinLvl0, 4 * sizeof(Fq2), 4 << 10));
-    if (G == 1) return part;
-    return sum_affine(allgather_affine(*C.comm, part));
+    const uint8_t* h = C.pin_at(Ctx::kPinLvl0, msm_out_bytes(true, 1), 4 << 10);
+    if (msm_status(h, true, 1) & kMsmOverflow) {
+        msm_ws_note_overflow(on_side ? C.msm_side : C.msm);
+        MsmShard sh = shard_of(comm);
+        sh.dense = true;
+        lvl0_launch(C, P, z, L, sh, on_side);
+        if (on_side)
+            C.side_sync();
+        else
+            C.sync();
+    }
+    return msm_results<HFq2>(comm, h, 1)[0];
 }
 
 // ---------------------------------------------------------------- open (open.rs:19-58)
@@ -698,105 +747,61 @@ struct OpenOut {
     HFr eval;
     std::vector<Affine<HFq2>> proofs;
 };
-// proof0: the shared level-0 proof (lvl0_launch/lvl0_finish), or null to compute every level here
-static OpenOut open_z(Ctx& C, PP& P, const Fr* z_local, int L, const std::vector<HFr>& point, int G, int rank,
+// Every level's quotient and fold run here on the whole table (also on proof-sharded ranks, which
+// all hold z: the folds are HBM-streaming and cheap, and the bucket-range MSM needs every scalar);
+// all MSMs of the opening are one batch. proof0: the shared level-0 proof (lvl0_launch /
+// lvl0_finish), or null to compute every level here.
+static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>& point, Comm& comm,
                       const Affine<HFq2>* proof0 = nullptr) {
-    const int g = ilog2((uint64_t)G);
-    const uint64_t nl = (1ull << L) / G;
-    const int nloc = L - g;  // local levels
-    if (proof0 && nloc < 1) proof0 = nullptr;
+    const uint64_t n = 1ull << L;
     const int first = proof0 ? 1 : 0;  // first level whose MSM runs here
     OpenOut res;
     res.proofs.resize(L);
     if (proof0) res.proofs[0] = *proof0;
     Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
-    Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * std::max<uint64_t>(nl, 1));
-    Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
-                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
+    Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * n);
+    Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(n / 2, 1)),
+                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(n / 4, 1))};
     uint8_t* ps = C.pin_at(Ctx::kPinStage, 32 * L, 64 << 10);
     memcpy(ps, point.data(), 32 * L);
     SPX_HIP(hipMemcpyAsync(pt, ps, 32 * L, hipMemcpyHostToDevice, C.stream));
-    std::vector<MsmInst> insts(nloc - first);
-    const Fr* rin = z_local;
+    std::vector<MsmInst> insts(L - first);
+    const Fr* rin = z;
     uint64_t qoff = 0;
-    for (int i = 0; i < nloc; ++i) {
-        const uint64_t half = nl >> (i + 1);
+    for (int i = 0; i < L; ++i) {
+        const uint64_t half = n >> (i + 1);
         Fr* rout = bufs[i & 1];
         launch_open_level(rin, rout, q + qoff, pt + i, half, C.stream);
-        if (i < first) {  // fold only; the level's proof is proof0 (its quotient is overwritten next)
-            rin = rout;
-            continue;
-        }
+        rin = rout;
+        if (i < first) continue;  // fold only; the level's proof is proof0 (its quotient is overwritten next)
         MsmInst& I = insts[i - first];
-        const uint64_t full = 1ull << (L - i - 1);
-        I.pts_off = P.g2_off[i] + (uint64_t)rank * half;
-        I.stride = (uint32_t)full;
+        I.pts_off = P.g2_off[i];
+        I.stride = (uint32_t)half;
         I.scalar_off = qoff;
         I.size = (uint32_t)half;
         I.c = (uint32_t)P.g2_c[i];
         I.W = (uint32_t)P.g2_W[i];
         qoff += half;
-        rin = rout;
     }
-    const int nm = nloc - first;  // MSMs of this batch
-    void* out = C.buf(Ctx::kSlotOpenOut, 4 * sizeof(Fq2) * std::max(nm, 1));
-    msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream);
-    const size_t xb = 4 * sizeof(Fq2);
-    uint8_t* h = C.pin_at(Ctx::kPinOpen, xb * nm + 32, 56 << 10);
-    if (nm) SPX_HIP(hipMemcpyAsync(h, out, xb * nm, hipMemcpyDeviceToHost, C.stream));
-    SPX_HIP(hipMemcpyAsync(h + xb * nm, rin, 32, hipMemcpyDeviceToHost, C.stream));
-    C.sync();
-    std::vector<Affine<HFq2>> part(nm);
-    for (int k = 0; k < nm; ++k) part[k] = xyzz_bytes_to_affine<HFq2>(h + xb * k);
-    HFr rlast = ld_hfr(h + xb * nm);
-    if (G == 1) {
-        for (int k = 0; k < nm; ++k) res.proofs[first + k] = part[k];
-        res.eval = rlast;
-        return res;
-    }
-    // gather partial proofs and the one remaining local value per rank
-    if (nm) {
-        std::vector<Affine<HFq2>> all((size_t)nm * G);
-        C.comm->allgather(part.data(), all.data(), sizeof(Affine<HFq2>) * nm);
-        for (int k = 0; k < nm; ++k) {
-            std::vector<Affine<HFq2>> v(G);
-            for (int r = 0; r < G; ++r) v[r] = all[(size_t)r * nm + k];
-            res.proofs[first + k] = sum_affine(v);
+    const int nm = L - first;  // MSMs of this batch
+    const size_t ob = msm_out_bytes(true, nm);
+    void* out = C.buf(Ctx::kSlotOpenOut, ob);
+    uint8_t* h = C.pin_at(Ctx::kPinOpen, ob + 32, 56 << 10);
+    for (int attempt = 0;; ++attempt) {
+        MsmShard sh = shard_of(comm);
+        sh.dense = attempt > 0;
+        if (nm) {
+            msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream, sh);
+            SPX_HIP(hipMemcpyAsync(h, out, ob, hipMemcpyDeviceToHost, C.stream));
         }
+        if (!attempt) SPX_HIP(hipMemcpyAsync(h + ob, rin, 32, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+        if (!nm || !(msm_status(h, true, nm) & kMsmOverflow)) break;
+        msm_ws_note_overflow(C.msm);  // compacted keys overflowed: once more with a slot per digit
     }
-    std::vector<HFr> rg = allgather_fr(*C.comm, {rlast});  // global r_g table (G entries)
-    // remaining g levels on the gathered table; tiny MSMs run redundantly on every rank
-    std::vector<HFr> qs;
-    std::vector<MsmInst> tinsts;
-    for (int i = nloc; i < L; ++i) {
-        const uint64_t half = rg.size() / 2;
-        std::vector<HFr> nr(half);
-        MsmInst I{};
-        I.pts_off = P.g2_off[i];
-        I.stride = (uint32_t)half;
-        I.scalar_off = qs.size();
-        I.size = (uint32_t)half;
-        I.c = (uint32_t)P.g2_c[i];
-        I.W = (uint32_t)P.g2_W[i];
-        for (uint64_t b = 0; b < half; ++b) {
-            HFr qq = rg[2 * b + 1] - rg[2 * b];
-            qs.push_back(qq);
-            nr[b] = rg[2 * b] + point[i] * qq;
-        }
-        rg.swap(nr);
-        tinsts.push_back(I);
-    }
-    res.eval = rg[0];
-    Fr* qd = C.buf<Fr>(Ctx::kSlotTailQ, 32 * qs.size());
-    void* out2 = C.buf(Ctx::kSlotTailOut, xb * tinsts.size());
-    uint8_t* hq = C.pin_at(Ctx::kPinTailIn, 32 * qs.size(), 32 << 10);
-    memcpy(hq, qs.data(), 32 * qs.size());
-    SPX_HIP(hipMemcpyAsync(qd, hq, 32 * qs.size(), hipMemcpyHostToDevice, C.stream));
-    msm_run_g2(C.msm, tinsts.data(), (int)tinsts.size(), P.g2_pre.as<G2Aff>(), qd, out2, C.stream);
-    uint8_t* h2 = C.pin_at(Ctx::kPinTailOut, xb * tinsts.size(), 32 << 10);
-    SPX_HIP(hipMemcpyAsync(h2, out2, xb * tinsts.size(), hipMemcpyDeviceToHost, C.stream));
-    C.sync();
-    for (size_t k = 0; k < tinsts.size(); ++k) res.proofs[nloc + k] = xyzz_bytes_to_affine<HFq2>(h2 + xb * k);
+    res.eval = ld_hfr(h + ob);
+    std::vector<Affine<HFq2>> part = msm_results<HFq2>(comm, h, nm);
+    for (int k = 0; k < nm; ++k) res.proofs[first + k] = part[k];
     return res;
 }
 
@@ -885,6 +890,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     if (!is_pow2(nvv)) invalid("public input should be power of two");
     if (W.n != n) invalid("|v| + |w| != number of variables");  // prover.rs:117-119
     if (!o.stub && !P) invalid("null public parameter");
+    C.side_sync();  // a proof that threw may have left its level-0 MSM running on the second stream
     if (P && P->nv != L) invalid("public parameter nv != log_n");
     const int log_v = ilog2(nvv);
     const Fr* z = W.z.as<Fr>();
@@ -931,23 +937,20 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // The shared level-0 opening proof is launched right behind the commitment, before any challenge,
     // when the host has the matrix absorption to do meanwhile. With the index-cached transcript there
     // is nothing to hide it behind: it then runs on the context's second stream, beside the commitment
-    // and the first opening, and is reused by the second opening (SPX_LVL0_SIDE=0: inside the first
-    // opening's batch instead, one MSM pipeline less on the critical path).
-    const bool share0 = !o.stub && lvl0_local(L, G);
+    // and the first opening, and is reused by the second opening. (Both forms give every rank the same
+    // batches, so the exchanges of a proof-sharded prove line up.)
+    const bool share0 = !o.stub;
     const bool early0 = share0 && !(o.cached && I.has_cache);
-    static const bool side_ok = [] {
-        const char* e = getenv("SPX_LVL0_SIDE");
-        return !(e && e[0] == '0');
-    }();
-    const bool side0 = share0 && !early0 && side_ok;
+    const bool side0 = share0 && !early0;
+    const MsmShard sh = shard_of(comm);
     if (side0) {  // z is in place: the second stream may start
         C.ensure_side();
         SPX_HIP(hipEventRecord(C.side_ev, C.stream));
     }
     // ---- round 1: commitment (prover.rs:123-141); the MSM runs while the host absorbs A, B, C
-    if (!o.stub) commit_launch(C, *P, z, n, G, rank);
-    if (early0) lvl0_launch(C, *P, zl, L, G, rank);
-    if (side0) lvl0_launch(C, *P, zl, L, G, rank, true);
+    if (!o.stub) commit_launch(C, *P, z, n, sh);
+    if (early0) lvl0_launch(C, *P, z, L, sh);
+    if (side0) lvl0_launch(C, *P, z, L, sh, true);
     Transcript T(o.mode == 1, o.seed);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
@@ -975,9 +978,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         T.feed(s.b.data(), s.b.size());
     }
     mark("transcript_matrices", tp);
-    Affine<HFq> com = o.stub ? Affine<HFq>{HFq::zero(), HFq::zero(), true} : commit_finish(C, G);
+    Affine<HFq> com = o.stub ? Affine<HFq>{HFq::zero(), HFq::zero(), true} : commit_finish(C, *P, z, n, comm);
     Affine<HFq2> proof0{};
-    if (early0) proof0 = lvl0_finish(C, G);
+    if (early0) proof0 = lvl0_finish(C, *P, z, L, comm);
     Ser proof;
     {
         size_t m0 = proof.b.size();
@@ -992,10 +995,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G)
-                            : open_z(C, *P, zl, L, pt1, G, rank, (early0 || side0) ? &proof0 : nullptr);
-        if (side0) op.proofs[0] = proof0 = lvl0_finish(C, G, true);
-        if (share0 && !early0) proof0 = op.proofs[0];
+        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, z, L, pt1, comm, share0 ? &proof0 : nullptr);
+        if (side0) op.proofs[0] = proof0 = lvl0_finish(C, *P, z, L, comm, true);
         size_t m0 = proof.b.size();
         ser_open(proof, op.eval, h_of(P), op.proofs);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
@@ -1223,7 +1224,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     mark("sumcheck2", tp);
     // ---- round 6: open at r_y (prover.rs:268-281)
     {
-        OpenOut op = o.stub ? open_stub(C, zl, L, r_y, G) : open_z(C, *P, zl, L, r_y, G, rank, share0 ? &proof0 : nullptr);
+        OpenOut op = o.stub ? open_stub(C, zl, L, r_y, G) : open_z(C, *P, z, L, r_y, comm, share0 ? &proof0 : nullptr);
         ser_open(proof, op.eval, h_of(P), op.proofs);
     }
     mark("open_ry", tp);
@@ -1621,7 +1622,7 @@ std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t*
     I.W = (uint32_t)windows_for((int)I.c);
     I.size = (uint32_t)n;
     I.stride = (uint32_t)n;
-    DevMem pre((g2 ? sizeof(G2Aff) : sizeof(G1Slot)) * n * I.W), out(4 * (g2 ? sizeof(Fq2) : sizeof(Fq)));
+    DevMem pre((g2 ? sizeof(G2Aff) : sizeof(G1Slot)) * n * I.W), out(msm_out_bytes(g2, 1));
     if (g2)
         precompute_level(C, raw.as<G2Aff>(), n, false, (int)I.c, (int)I.W, pre.as<G2Aff>());
     else
@@ -1638,17 +1639,20 @@ std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t*
     if (herr & 1) throw SpxError(kSerialization, "non-canonical input");
     if (herr & 2) throw SpxError(kSerialization, "base point not on the curve");
     std::vector<uint8_t> res(ps);
+    LocalComm local;
     if (g2)
-        host::g2_to_uncompressed(res.data(), xyzz_bytes_to_affine<HFq2>(h.data()));
+        host::g2_to_uncompressed(res.data(), msm_results<HFq2>(local, h.data(), 1)[0]);
     else
-        host::g1_to_uncompressed(res.data(), xyzz_bytes_to_affine<HFq>(h.data()));
+        host::g1_to_uncompressed(res.data(), msm_results<HFq>(local, h.data(), 1)[0]);
     return res;
 }
 
 std::vector<uint8_t> k_commit(Ctx& C, PP& P, const uint8_t* table, int nv) {
     if (nv != P.nv) invalid("table size != 2^nv of the public parameters");
     auto W = witness_upload(C, table, 1, table + 32, (1ull << nv) - 1);
-    Affine<HFq> a = commit_z(C, P, W->z.as<Fr>(), 1ull << nv, 1, 0);
+    LocalComm local;
+    commit_launch(C, P, W->z.as<Fr>(), 1ull << nv, MsmShard());
+    Affine<HFq> a = commit_finish(C, P, W->z.as<Fr>(), 1ull << nv, local);
     std::vector<uint8_t> out(56);
     uint64_t u = (uint64_t)nv;
     memcpy(out.data(), &u, 8);
@@ -1662,7 +1666,8 @@ std::vector<uint8_t> k_open(Ctx& C, PP& P, const uint8_t* table, int nv, const u
     std::vector<HFr> pt(nv);
     for (int i = 0; i < nv; ++i)
         if (!host::fr_from_bytes(pt[i], point + 32 * i)) throw SpxError(kSerialization, "non-canonical point");
-    OpenOut op = open_z(C, P, W->z.as<Fr>(), nv, pt, 1, 0);
+    LocalComm local;
+    OpenOut op = open_z(C, P, W->z.as<Fr>(), nv, pt, local);
     Ser s;
     ser_open(s, op.eval, P.h, op.proofs);
     return s.b;

@@ -134,19 +134,17 @@ struct Ctx {
     // stream sync that covers the copies issued from it.
     enum : size_t {
         kPinHp = 0,                 // prove(): challenges up, round results down (64 KiB)
-        kPinCommit = 64 << 10,      // commitment MSM result (4 KiB)
-        kPinLvl0 = 68 << 10,        // shared level-0 opening proof (4 KiB)
-        kPinOpen = 72 << 10,        // opening results / evaluations (56 KiB)
-        kPinTailIn = 128 << 10,     // last g opening levels: quotients up (32 KiB)
-        kPinTailOut = 160 << 10,    // ... and their MSM results down (32 KiB)
-        kPinStage = 192 << 10,      // small host-to-device staging (opening points, constants) (64 KiB)
-        kPinBytes = 256 << 10
+        kPinCommit = 64 << 10,      // commitment MSM result + status (4 KiB)
+        kPinLvl0 = 68 << 10,        // shared level-0 opening proof + status (4 KiB)
+        kPinOpen = 72 << 10,        // opening results + status / evaluations (56 KiB)
+        kPinStage = 128 << 10,      // small host-to-device staging (opening points, constants) (64 KiB)
+        kPinBytes = 192 << 10
     };
     uint8_t* pin = nullptr;
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
-    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotTailQ, kSlotTailOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
+    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
     DevMem slot[kSlots];
     template <class T = void>
     T* buf(int id, size_t bytes) {
@@ -160,9 +158,15 @@ struct Ctx {
     ~Ctx();
     // region [off, off + bytes) of the pinned carve-out (throws if it does not fit its region)
     uint8_t* pin_at(size_t off, size_t bytes, size_t region);
-    void sync() {
+    void sync() {  // the main stream's work is done: its MSM staging may be reused
         SPX_HIP(hipStreamSynchronize(stream));
+        msm_ws_staging_reset(msm);
         if (kprof.on) kprof.harvest();
+    }
+    void side_sync() {
+        if (!side) return;
+        SPX_HIP(hipStreamSynchronize(side));
+        msm_ws_staging_reset(msm_side);
     }
 };
 

@@ -1,6 +1,9 @@
 """The product's sharded path (prover.cpp) on ONE GPU: G in-process ranks (one host
 thread + context each, in-process communicator) must produce the single-rank proof byte for byte.
-RCCL itself is exercised by bench.py --gpus N on a multi-GPU node."""
+The MSMs split every instance by bucket range (MsmShard, kernels.hpp); the cases below also drive
+their compacted-key overflow and the dense rerun. RCCL itself is exercised by bench.py --gpus N on
+a multi-GPU node."""
+import os
 import threading
 
 import pytest
@@ -8,16 +11,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("G,kind,log_n", [(2, 0, 6), (4, 0, 8), (8, 2, 9), (2, 1, 10)])
-def test_virtual_ranks_equal_single(spx, oc, G, kind, log_n):
-    log_v = 3
-    param = (3 | (2 << 16)) if kind == 2 else 0
-    inst = oc.Instance(kind, log_n, log_v, 300 + log_n, param)
-    ppb = oc.PP.keygen(log_n, 400 + log_n).serialize()
-    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
+def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
     group = spx.CommGroup(G)
     out = [None] * G
     errs = []
+    w = inst.w_bytes if w_bytes is None else w_bytes
 
     def run(r):
         try:
@@ -26,7 +24,7 @@ def test_virtual_ranks_equal_single(spx, oc, G, kind, log_n):
             pp = spx.PublicParameter.load(ctx, ppb)
             mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
             pk = spx.MLArgumentForR1CS.index(ctx, *mats)
-            out[r] = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+            out[r] = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, w, pp)
         except Exception as e:  # surfaced below
             errs.append(repr(e))
 
@@ -36,5 +34,46 @@ def test_virtual_ranks_equal_single(spx, oc, G, kind, log_n):
     for t in ths:
         t.join(timeout=600)
     assert not errs, errs
+    return out
+
+
+@pytest.mark.parametrize("G,kind,log_n", [(2, 0, 6), (4, 0, 8), (8, 2, 9), (2, 1, 10), (8, 0, 12)])
+def test_virtual_ranks_equal_single(spx, oc, G, kind, log_n):
+    log_v = 3
+    param = (3 | (2 << 16)) if kind == 2 else 0
+    inst = oc.Instance(kind, log_n, log_v, 300 + log_n, param)
+    ppb = oc.PP.keygen(log_n, 400 + log_n).serialize()
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
+    out = _prove_ranks(spx, G, inst, ppb)
     for r in range(G):
         assert out[r] == want, "rank %d proof differs" % r
+
+
+def test_virtual_ranks_forced_key_overflow(spx, oc):
+    """SPX_MSM_CAP_SCALE=0.5 halves the compacted-key capacity: the first batches of every rank
+    overflow, are rerun with one key slot per digit, and the proof stays byte-identical."""
+    log_n, log_v, G = 10, 3, 4
+    inst = oc.Instance(0, log_n, log_v, 900 + log_n, 0)
+    ppb = oc.PP.keygen(log_n, 901).serialize()
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
+    os.environ["SPX_MSM_CAP_SCALE"] = "0.5"
+    try:
+        out = _prove_ranks(spx, G, inst, ppb)
+    finally:
+        del os.environ["SPX_MSM_CAP_SCALE"]
+    assert all(p == want for p in out)
+
+
+@pytest.mark.parametrize("fill", [1, 0])
+def test_virtual_ranks_crowded_buckets(spx, oc, fill):
+    """a witness of equal values: every commitment digit lands in one bucket (one rank's range:
+    its compacted keys overflow and the batch is rerun dense), every opening quotient is 0. The
+    proof is not a valid one (the witness does not satisfy the matrices); it must still equal the
+    oracle's byte for byte."""
+    log_n, log_v, G = 9, 3, 4
+    inst = oc.Instance(0, log_n, log_v, 950 + log_n, 0)
+    ppb = oc.PP.keygen(log_n, 951).serialize()
+    w = fill.to_bytes(32, "little") * ((1 << log_n) - (1 << log_v))
+    want = oc.prove(inst.mats, inst.v_bytes, w, oc.PP.load(ppb), 0, 0)
+    out = _prove_ranks(spx, G, inst, ppb, w)
+    assert all(p == want for p in out)

@@ -350,8 +350,9 @@ def main():
     ap.add_argument("--kind", type=int, default=3, help="3 circuit-3n (distinct witnesses), 0 uniform-3n, 1 ref-shaped")
     ap.add_argument("--witnesses", type=int, default=0, help="distinct witnesses (kind 3; default: one per proof of a step)")
     ap.add_argument("--mode", default="fs", choices=["fs", "injected"])
-    ap.add_argument("--cpu-log-n", type=int, default=14, help="1-core CPU baseline sample size")
-    ap.add_argument("--cpu-all-log-n", type=int, default=18, help="all-cores CPU baseline sample size")
+    ap.add_argument("--cpu-log-n", type=int, default=16, help="1-core CPU baseline sample size (one proof ~17 s)")
+    ap.add_argument("--cpu-all-log-n", type=int, default=20,
+                    help="all-cores CPU baseline sample size (default: the metric's 2^20, one proof ~30 s on 16 cores)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
@@ -563,16 +564,23 @@ def main():
                     roof["whole_proof"] = wp
     cpu = cpu_all = None
     if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.kind, args.cpu_log_n if not stub else 16, log_v, args.cpu_seconds, stub=stub)
-        pp_bytes = None
-        if not stub and args.cpu_all_log_n != args.cpu_log_n:
-            # the GPU keygen's PP at the all-cores sample size, loaded into the oracle (CPU keygen at 2^18+
-            # would dominate the run)
-            pp_s = spx.MLProofForR1CS.setup(ctx, args.cpu_all_log_n, 0xC0FFEE)
-            pp_bytes = pp_s.serialize_uncompressed()
+        def gpu_pp_bytes(k):
+            # the GPU keygen's PP (seed 0xC0FFEE, as the oracle's keygen would make it), loaded into the
+            # oracle: a CPU keygen at 2^16+ would dominate the run
+            if k == log_n and pp is not None:
+                return pp.serialize_uncompressed()
+            pp_s = spx.MLProofForR1CS.setup(ctx, k, 0xC0FFEE)
+            b = pp_s.serialize_uncompressed()
             del pp_s
-        cpu_all = cpu_baseline(args.kind, args.cpu_all_log_n if not stub else log_n, log_v, args.cpu_seconds,
-                               threads=host_cores(), pp_bytes=pp_bytes, stub=stub, max_reps=1)
+            return b
+
+        one_log_n = args.cpu_log_n if not stub else 16
+        cpu = cpu_baseline(args.kind, one_log_n, log_v, args.cpu_seconds, stub=stub, max_reps=1,
+                           pp_bytes=None if stub else gpu_pp_bytes(one_log_n))
+        all_log_n = args.cpu_all_log_n if not stub else log_n
+        pp_bytes = None if stub else gpu_pp_bytes(all_log_n)
+        cpu_all = cpu_baseline(args.kind, all_log_n, log_v, args.cpu_seconds, threads=host_cores(), pp_bytes=pp_bytes,
+                               stub=stub, max_reps=1)
         del pp_bytes
     wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
         KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
@@ -620,6 +628,12 @@ def main():
         "gen_s": round(t_gen, 2),
         "proof_bytes": len(ref[0]),
     }
+    # host side: the machine's cores, the ones this process uses, and how many of them the per-proof
+    # sequential Blake2s absorption of A, B, C keeps busy at the measured rate (proofs/s x seconds each)
+    hash_s = phases.get("transcript_matrices", 0.0) / 1e6
+    out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
+                   "hashing_s_per_proof": round(hash_s, 4),
+                   "hashing_cores_busy": round(jobs / (ms / 1e3) * hash_s, 2)}
     if ms_o is not None:
         if sharded_head:  # the other mode: every rank proves whole proofs
             out["value_batch_weak"] = round(P * world * n / (ms_o / 1e3), 1)

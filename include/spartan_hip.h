@@ -92,6 +92,10 @@ int spx_comm_shm_destroy(void *comm);
 int spx_comm_group_create(int world, void **group_out);
 int spx_comm_group_destroy(void *group);
 int spx_ctx_set_comm_group(spx_ctx *ctx, void *group, int rank);
+/* Rehearsal: this context acts as rank `rank` of a `world`-rank proof-sharded prove WITHOUT peers
+ * (every exchange returns its own contribution in all slots): the device and host work of one rank
+ * on a GPU of its own, for throughput estimates of an N-GPU node. Its proofs are not valid. */
+int spx_ctx_set_comm_rehearsal(spx_ctx *ctx, int rank, int world);
 /* one allgather on the context's communicator (whatever its transport): every rank passes `bytes`,
  * recv receives world * bytes in rank order. For transport tests. */
 int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t bytes);
@@ -200,6 +204,10 @@ int spx_kernel_stats_largest(spx_ctx *ctx, int id, uint64_t *launches, double *m
 /* unit operations counted for a kernel id: curve additions (upper bound: zero digits included) for
  * SPX_K_ACC_* (mixed) and SPX_K_ACCX_* (XYZZ); 0 for the others */
 int spx_kernel_ops(spx_ctx *ctx, int id, double *ops);
+/* MSM batches of this context rerun with one key slot per digit because a proof-sharded rank's
+ * compacted keys overflowed their planned capacity (scalars crowding one rank's buckets); a
+ * diagnostic: the results are exact either way */
+int spx_msm_reruns(spx_ctx *ctx, uint64_t *reruns);
 
 /* ---- kernel-level entry points (parity tests) ---- */
 int spx_sum_over_y(spx_ctx *ctx, const spx_csr *m, const uint8_t *z, uint8_t *out);

@@ -82,6 +82,7 @@ EXPORTED = [
     "spx_comm_group_create",
     "spx_comm_group_destroy",
     "spx_ctx_set_comm_group",
+    "spx_ctx_set_comm_rehearsal",
     "spx_ctx_comm_allgather",
     "spx_pp_load",
     "spx_pp_generate",
@@ -143,6 +144,7 @@ def lib():
     L.spx_comm_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
+    L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.spx_ctx_comm_allgather.argtypes = [vp, ctypes.c_char_p, ctypes.c_void_p, sz]
     L.spx_pp_load.argtypes = [vp, u8p, sz, ctypes.POINTER(vp)]
     L.spx_pp_generate.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
@@ -265,12 +267,23 @@ class Context:
     def set_comm_group(self, group, rank):
         _check(lib().spx_ctx_set_comm_group(self.h, group.h, int(rank)))
 
+    def set_comm_rehearsal(self, rank, world):
+        """one rank of a world-rank proof-sharded prove without its peers (throughput rehearsal; the
+        proofs are not valid)"""
+        _check(lib().spx_ctx_set_comm_rehearsal(self.h, int(rank), int(world)))
+
     def comm_allgather(self, data, world):
         """one allgather of `data` on this context's communicator -> list of world byte strings"""
         data = bytes(data)
         out = ctypes.create_string_buffer(max(1, len(data) * world))
         _check(lib().spx_ctx_comm_allgather(self.h, data, out, len(data)))
         return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(world)]
+
+    def msm_reruns(self):
+        """MSM batches rerun with dense keys after a compacted-key overflow (spx_msm_reruns)"""
+        v = ctypes.c_uint64(0)
+        _check(lib().spx_msm_reruns(self.h, ctypes.byref(v)))
+        return v.value
 
     def last_timings(self):
         buf = (ctypes.c_double * 32)()

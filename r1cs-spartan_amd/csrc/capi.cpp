@@ -164,6 +164,14 @@ int spx_ctx_set_comm_group(spx_ctx* ctx, void* group, int rank) {
     });
 }
 
+int spx_ctx_set_comm_rehearsal(spx_ctx* ctx, int rank, int world) {
+    return guard([&] {
+        if (!ctx) spx::invalid("null context");
+        if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
+        ctx->c->comm.reset(new spx::SoloComm(rank, world));
+    });
+}
+
 int spx_ctx_comm_allgather(spx_ctx* ctx, const void* send, void* recv, size_t bytes) {
     return guard([&] {
         set_dev(ctx);
@@ -428,6 +436,12 @@ int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
         set_dev(ctx);
         ctx->c->sync();
         if (ops) *ops = ctx->c->kprof.ops[id];
+    });
+}
+int spx_msm_reruns(spx_ctx* ctx, uint64_t* reruns) {
+    return guard([&] {
+        if (!ctx || !reruns) spx::invalid("null argument");
+        *reruns = ctx->c->msm_reruns.load();
     });
 }
 int spx_sum_over_y(spx_ctx* ctx, const spx_csr* m, const uint8_t* z, uint8_t* out) {

@@ -35,7 +35,8 @@ namespace spx {
 namespace {
 constexpr int kMaxRanks = 64;
 constexpr size_t kSlot = 1 << 16;
-constexpr size_t kHdr = 64 * kMaxRanks;
+constexpr size_t kEpoch = 64 * kMaxRanks;  // one line after the counters: rank 0's per-run epoch
+constexpr size_t kHdr = kEpoch + 64;
 }  // namespace
 
 struct ShmComm : Comm {
@@ -80,11 +81,37 @@ struct ShmComm : Comm {
         close(fd);
         if (p == MAP_FAILED) throw SpxError(kDevice, "mmap failed for " + name);
         base = (uint8_t*)p;
+        // Rank 0 stamps a per-run epoch into the fresh (zero-filled) segment; the others wait for it.
+        // A segment left behind by a crashed run is refused: its counters are past the rendezvous,
+        // or its epoch is not the one the live rank 0 wrote (checked after the rendezvous).
+        auto& epoch = *reinterpret_cast<std::atomic<uint64_t>*>(base + kEpoch);
+        if (r == 0) {
+            uint64_t e = 0;
+            while (!e) e = ((uint64_t)getpid() << 32) ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+            epoch.store(e, std::memory_order_release);
+        } else {
+            auto t0 = std::chrono::steady_clock::now();
+            while (!epoch.load(std::memory_order_acquire)) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
+                    throw SpxError(kDevice, "shm comm: segment " + name + " never initialised by rank 0");
+                usleep(100);
+            }
+            for (int k = 0; k < world; ++k)
+                if (!reached(1, seq(k).load(std::memory_order_acquire)))
+                    throw SpxError(kDevice, "shm comm: segment " + name + " is in use by another run (stale name?)");
+        }
+        const uint64_t mine = epoch.load(std::memory_order_acquire);
         // rendezvous: every rank has mapped the segment once this completes; then drop the name
-        std::vector<int> ranks(world);
-        allgather(&r, ranks.data(), sizeof(int));
+        struct Hello {
+            int rank;
+            int pad;
+            uint64_t epoch;
+        } hello{r, 0, mine};
+        std::vector<Hello> all(world);
+        allgather(&hello, all.data(), sizeof(Hello));
         for (int k = 0; k < world; ++k)
-            if (ranks[k] != k) throw SpxError(kDevice, "shm comm: rank mismatch (stale segment name?)");
+            if (all[k].rank != k || all[k].epoch != all[0].epoch)
+                throw SpxError(kDevice, "shm comm: rank / epoch mismatch (stale segment name?)");
         if (r == 0) shm_unlink(name.c_str());
     }
     ~ShmComm() override {

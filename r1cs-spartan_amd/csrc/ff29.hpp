@@ -137,10 +137,14 @@ DEV void f29_redc_sum(F29& r, const F29* const (&a)[NP], const F29* const (&b)[N
 
 // r = REDC(a0 b0 + a1 b1 + a2 b2 + a3 b3): one reduction for four products. A column then holds up
 // to 4 x 14 products and 14 m p terms, which can pass 2^64, so it is summed in two 64-bit chains
-// (A: products 0, 1; B: products 2, 3 and m p), each below 2^64 as long as every product is below
-// 2^59 (limbs < 2^29, or one factor's limbs < 2^30 as in the borrow-free lane-pair operands):
-// A <= 28 x 2^59, B <= 28 x 2^59 + 14 x 2^58. The chains are joined without a 65-bit sum: the column's
-// low 29 bits come from the low parts, the carry from the high parts plus the low parts' overflow.
+// (A: products 0, 1; B: products 2, 3 and m p). PRECONDITION: in each chain at most ONE of its two
+// products may have a factor with limbs below 2^30 (limb products < 2^59, as the borrow-free
+// lane-pair operands give); the other product must have both factors' limbs below 2^29 (< 2^58).
+// Then A <= 14 x 2^59 + 14 x 2^58 = 42 x 2^58 and B <= 14 x 2^59 + 14 x 2^58 + 14 x 2^58 (m p)
+// = 56 x 2^58, both below 2^64 = 64 x 2^58; two 2^30-limb products in one chain (70 x 2^58 with m p)
+// would overflow. The only caller, PairOps<FP29A>::mul_sum (fq2pair.hpp), meets it. The chains are
+// joined without a 65-bit sum: the column's low 29 bits come from the low parts, the carry from the
+// high parts plus the low parts' overflow.
 DEV void f29_redc_sum4(F29& r, const F29& a0, const F29& b0, const F29& a1, const F29& b1, const F29& a2,
                        const F29& b2, const F29& a3, const F29& b3) {
     uint32_t m[14], t[14];

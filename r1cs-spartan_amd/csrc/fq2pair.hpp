@@ -113,6 +113,8 @@ struct PairOps {
                 const uint32_t zd = pair_odd_val(d.v.v[i]);
                 z2.v[i] = (zd ^ msk) + (msk & (k16(i) + 1u));
             }
+            // chains (a y1, ap y2) and (c z1, cp z2): one factor with 2^30 limbs (y2, z2) per chain, the
+            // precondition of f29_redc_sum4
             f29_redc_sum4(r.v, a.v, y1, ap, y2, c.v, z1, cp, z2);
         } else {
             P x, y;

@@ -124,11 +124,14 @@ void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* 
 void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
                      Fr* scratch_hi, hipStream_t s);
 int sc_grid(uint64_t half);
-void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr* r,
-                      uint64_t half, Fr* partial, Fr* result3, hipStream_t s);
-void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr* r, uint64_t half,
-                      Fr* partial, Fr* result3, hipStream_t s);
-void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s);
+// One launch per round: fold with the previous challenge r (by value; unused in round 1), evaluate the
+// round polynomial at 0, 1, 2, and reduce over the blocks into result3 (3 Fr; device or host-mapped
+// pinned memory). partial: sc_grid(half) x 3 Fr of scratch; ticket: a device counter that is 0 (left 0).
+void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
+                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s);
+void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
+                      Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s);
+void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
 
 // ---- msm.hip
 // One MSM inside a batch. Bases are the PRECOMPUTED window copies of a base set:
@@ -142,17 +145,19 @@ struct MsmInst {
     // filled in by the MSM driver:
     uint32_t bucket_off;  // first local bucket of this instance
     uint32_t ref_off;     // first (bucket, reference) slot of this instance (dense key layout)
-    uint32_t lb;          // log2 of the buckets this rank weights: c - 1 (whole) or c - 1 - log2(world) (split)
-    uint32_t sel;         // this rank's bucket range [sel << lb, (sel + 1) << lb) of the 2^(c-1)
+    uint32_t lb;          // log2 of the buckets this rank weights: c - 1 (whole) or c - 1 - lg (split)
+    uint32_t lg;          // split: this rank weights buckets u = sel + 2^lg k (u = |digit| - 1); whole: 0
+    uint32_t sel;
     uint32_t out;         // output slot (index in the caller's instance list)
-    uint32_t pad;
 };
 
-// Bucket-range partition of a batch over the ranks of a proof-sharded prove: every
-// rank reads ALL scalars of an instance and keeps the digits whose bucket lies in its range, so the
-// accumulation, the partial levels and the bucket weighting all divide by the world size. Rank r's
-// result for an instance is sum_{j in its range} (j + 1) S_j; the ranks' results sum to the MSM.
-// Instances too small to split (fewer than 4 buckets per rank) go whole to rank (index mod world).
+// Bucket partition of a batch over the ranks of a proof-sharded prove: every rank
+// reads ALL scalars of an instance and keeps the digits whose bucket is one of its own, so the
+// accumulation, the partial levels and the bucket weighting all divide by the world size. Buckets
+// are dealt round-robin (rank r: u = r, r + G, r + 2G, ...): the digits of the top windows, which
+// crowd the low buckets (scalars < r < 2^255), spread evenly over the ranks. Rank r's result for an
+// instance is sum_{its u} (u + 1) S_u; the ranks' results sum to the MSM. Instances too small to
+// split (fewer than 4 buckets per rank) go whole to rank (index mod world).
 struct MsmShard {
     int rank = 0, world = 1;
     bool dense = false;  // world > 1: one key slot per (scalar, window), as at world 1 (never overflows)

@@ -7,8 +7,10 @@
 //   * sumcheck rounds (AHPForMLSumcheck::prove_round [upstream]) fused with the binding of the
 //     previous challenge, and the mKZG quotient/fold levels of open.rs:37-45.
 // Every kernel is a grid-stride stream over 32-byte Fr elements (two 16-byte loads per element),
-// with per-block partial sums reduced by wave64 shuffles + LDS and a second one-block pass:
-// the reduction order is fixed, and field addition is exact, so results are deterministic.
+// with per-block partial sums reduced by wave64 shuffles + LDS and, in the last block to finish,
+// over the blocks (field addition is exact, so results are deterministic). A sumcheck round is ONE
+// launch: the previous challenge arrives as a kernel argument and the round's three sums are written
+// straight into the host's pinned memory.
 #include "kernels.hpp"
 
 #include <stdexcept>
@@ -65,6 +67,38 @@ __global__ __launch_bounds__(kThreads) void k_reduce_partials(const Fr* __restri
         for (int k = 0; k < K; ++k) fe_add(acc[k], acc[k], ld_fr(partial + (size_t)b * K + k));
     }
     block_reduce_store<K>(acc, out);
+}
+
+// Last-block reduction (one launch per sumcheck round instead of two): every block stores its K
+// partials, then takes a ticket; the block drawing the last ticket sums all partials in block order
+// (field addition is exact: the same element as k_reduce_partials) into `out` (may be host-mapped
+// pinned memory, read by the host after the stream sync) and resets the ticket for the next launch.
+template <int K>
+DEV void grid_reduce_last(Fr (&acc)[K], Fr* __restrict__ partial, uint32_t* __restrict__ ticket, Fr* __restrict__ out) {
+    block_reduce_store<K>(acc, partial + (size_t)blockIdx.x * K);
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        __threadfence();  // this block's partial is visible device-wide before its ticket
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // acquire: every other block's partial
+#pragma unroll
+    for (int k = 0; k < K; ++k) fe_zero(acc[k]);
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Fr v;
+            const Fr* src = partial + (size_t)b * K + k;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] = __builtin_nontemporal_load(&src->v[i]);
+            fe_add(acc[k], acc[k], v);
+        }
+    }
+    __syncthreads();  // the shared scratch of the first block_reduce_store is free again
+    block_reduce_store<K>(acc, out);
+    if (threadIdx.x == 0) *ticket = 0u;
 }
 
 // ------------------------------------------------------------------ conversions
@@ -215,10 +249,9 @@ __global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ l
 // partial[blk] = (G(0), G(1), G(2)) with G(t) = sum_b (A_t B_t - C_t) e,  X_2 = 2 X_1 - X_0.
 template <bool FOLD>
 __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
-                                                        Fr* __restrict__ Eout, const Fr* __restrict__ rch,
-                                                        uint64_t half, Fr* __restrict__ partial) {
-    Fr r;
-    if (FOLD) r = ld_fr(rch);
+                                                        Fr* __restrict__ Eout, const Fr r, uint64_t half,
+                                                        Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                                                        Fr* __restrict__ result3) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -273,18 +306,16 @@ __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out,
         fe_mul(t, t, e);
         fe_add(g[2], g[2], t);
     }
-    block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+    grid_reduce_last<3>(g, partial, ticket, result3);
 }
 
 // ------------------------------------------------------------------ sumcheck #2 round
 // tables M (= sum_m r_m M(r_x, .)) and Z; partial = (P(0), P(1), P(2)), P(t) = sum_b M_t Z_t.
 template <bool FOLD>
 __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
-                                                        Fr* __restrict__ Mout, Fr* __restrict__ Zout,
-                                                        const Fr* __restrict__ rch, uint64_t half,
-                                                        Fr* __restrict__ partial) {
-    Fr r;
-    if (FOLD) r = ld_fr(rch);
+                                                        Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
+                                                        uint64_t half, Fr* __restrict__ partial,
+                                                        uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -328,17 +359,14 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
         fe_mul(t, u, v);
         fe_add(g[2], g[2], t);
     }
-    block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+    grid_reduce_last<3>(g, partial, ticket, result3);
 }
 
 // ------------------------------------------------------------------ mKZG open level (open.rs:42-45)
 // q[b] = r[2b+1] - r[2b];  r'[b] = r[2b] + p * q[b]   ( = r[2b](1-p) + r[2b+1] p )
 // q may be null (fold only: the commitment-stubbed mode evaluates z without quotients)
 __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
-                                                         Fr* __restrict__ q, const Fr* __restrict__ point,
-                                                         uint64_t half) {
-    Fr p{};
-    if (rout) p = ld_fr(point);
+                                                         Fr* __restrict__ q, const Fr p, uint64_t half) {
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
         fe_sub(d, a1, a0);
@@ -404,32 +432,34 @@ void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* 
 
 int sc_grid(uint64_t half) { return grid_for(half, 1024); }
 
-void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr* r,
-                      uint64_t half, Fr* partial, Fr* result3, hipStream_t s) {
+void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
+                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC1, s);
     if (fold)
-        hipLaunchKernelGGL(k_sc1_round<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
+        hipLaunchKernelGGL(k_sc1_round<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial, ticket,
+                           result3);
     else
-        hipLaunchKernelGGL(k_sc1_round<false>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial);
+        hipLaunchKernelGGL(k_sc1_round<false>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial, ticket,
+                           result3);
     // algorithmic bytes: fold reads 4 Fr x 3 tables + 2 E, writes 2 x 3 + 1 E; no fold reads 2 x 3 + 1
     kp_end(32.0 * (double)half * (fold ? (14.0 + 6.0 + (Eout ? 1.0 : 0.0)) : 7.0), s);
-    hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
-void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr* r, uint64_t half,
-                      Fr* partial, Fr* result3, hipStream_t s) {
+void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
+                      Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC2, s);
     if (fold)
-        hipLaunchKernelGGL(k_sc2_round<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
+        hipLaunchKernelGGL(k_sc2_round<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
+                           ticket, result3);
     else
-        hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial);
+        hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
+                           ticket, result3);
     kp_end(32.0 * (double)half * (fold ? 12.0 : 4.0), s);
-    hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
-void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr* point, uint64_t half, hipStream_t s) {
+void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s) {
     kp_begin(KP_OPEN, s);
     hipLaunchKernelGGL(k_open_level, dim3(grid_for(half, 8192)), dim3(kThreads), 0, s, rin, rout, q, point, half);
     kp_end(32.0 * (2.0 + (q ? 1.0 : 0.0) + (rout ? 1.0 : 0.0)) * (double)half, s);  // read 2, write q and/or r'

@@ -49,27 +49,27 @@ struct Digits {
         return carry ? (int32_t)v - (int32_t)full : (int32_t)v;
     }
 };
-// the digit's bucket if it lies in this rank's range of the instance (local index in the batch), else ~0u
+// the digit's bucket if it is one of this rank's (local index in the batch), else ~0u
 DEV uint32_t digit_key(const MsmInst& I, int32_t d) {
     if (!d) return ~0u;
     const uint32_t u = (uint32_t)(d < 0 ? -d : d) - 1;  // 0 .. 2^(c-1) - 1
-    if ((u >> I.lb) != I.sel) return ~0u;
-    return I.bucket_off + (u & ((1u << I.lb) - 1));
+    if ((u & ((1u << I.lg) - 1)) != I.sel) return ~0u;
+    return I.bucket_off + (u >> I.lg);
 }
 DEV uint32_t digit_ref(const MsmInst& I, uint32_t w, uint64_t j, int32_t d) {
     return (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
 }
 
 // One thread per scalar. Dense: a (key, reference) pair for every (scalar, window), window-major
-// within each instance so the stores coalesce; digits that are zero or outside the rank's range get
-// the key nb and sort last. Compact (proof-sharded ranks): only in-range digits, appended through
-// a block-level scan and one atomic per block; pairs past `cap` are dropped and flag the status.
+// within each instance so the stores coalesce; digits that are zero or not this rank's get the key
+// nb and sort last. Compact (proof-sharded ranks): only this rank's digits, appended through a
+// block-level scan and one atomic per block (st[1]); pairs past `cap` are dropped and flag st[0];
+// the last block to finish (ticket st[2]) fills the unused key slots with ~0 (sorts last).
 template <bool COMPACT>
 __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
                                                      int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
-                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                     uint32_t* __restrict__ cursor, uint32_t cap,
-                                                     uint32_t* __restrict__ status) {
+                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t cap,
+                                                     uint32_t* __restrict__ st) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = g < total;
     if (!COMPACT && !live) return;
@@ -103,68 +103,92 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
         using Scan = hipcub::BlockScan<uint32_t, kLight>;
         __shared__ typename Scan::TempStorage tmp;
         __shared__ uint32_t base;
+        __shared__ bool last;
         uint32_t pre, agg;
         Scan(tmp).ExclusiveSum(cnt, pre, agg);
         if (threadIdx.x == 0) {
-            base = agg ? atomicAdd(cursor, agg) : 0u;
-            if ((uint64_t)base + agg > cap) atomicOr(status, kMsmOverflow);
+            base = agg ? atomicAdd(&st[1], agg) : 0u;
+            if ((uint64_t)base + agg > cap) atomicOr(&st[0], kMsmOverflow);
         }
         __syncthreads();
-        if (!cnt) return;
-        uint64_t pos = (uint64_t)base + pre;
-        Digits d = d0;
-        for (uint32_t w = 0; w < I.W; ++w) {
-            const int32_t dg = d.next(I.c);
-            const uint32_t key = digit_key(I, dg);
-            if (key == ~0u) continue;
-            if (pos < cap) {
-                keys[pos] = key;
-                vals[pos] = digit_ref(I, w, j, dg);
+        if (cnt) {
+            uint64_t pos = (uint64_t)base + pre;
+            Digits d = d0;
+            for (uint32_t w = 0; w < I.W; ++w) {
+                const int32_t dg = d.next(I.c);
+                const uint32_t key = digit_key(I, dg);
+                if (key == ~0u) continue;
+                if (pos < cap) {
+                    keys[pos] = key;
+                    vals[pos] = digit_ref(I, w, j, dg);
+                }
+                ++pos;
             }
-            ++pos;
+        }
+        if (threadIdx.x == 0) {
+            __threadfence();
+            last = atomicAdd(&st[2], 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last) {  // every block has taken its slots: fill the rest
+            const uint32_t used = min(atomicAdd(&st[1], 0u), cap);
+            for (uint32_t i = used + threadIdx.x; i < cap; i += blockDim.x) keys[i] = ~0u;
         }
     }
 }
-// sorted keys -> first index and end of every bucket's run (ends pre-zeroed; starts of empty buckets unset)
-__global__ __launch_bounds__(kLight) void k_bucket_runs(const uint32_t* __restrict__ keys, uint64_t n, uint32_t nb,
-                                                        uint32_t* __restrict__ offs, uint32_t* __restrict__ ends) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = keys[i];
-    if (k >= nb) return;
-    if (i == 0 || keys[i - 1] != k) offs[k] = (uint32_t)i;
-    if (i + 1 == n || keys[i + 1] != k) ends[k] = (uint32_t)(i + 1);
-}
-__global__ void k_bucket_counts(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ ends, uint32_t nb,
-                                uint32_t* __restrict__ cnt) {
+
+// sorted keys -> offs[b] = first index with key >= b, for b = 0..nb (offs[nb] = the references;
+// an empty bucket shares the next bucket's offset)
+__global__ __launch_bounds__(kLight) void k_bucket_bounds(const uint32_t* __restrict__ keys, uint64_t n, uint32_t nb,
+                                                          uint32_t* __restrict__ offs) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) cnt[b] = ends[b] ? ends[b] - offs[b] : 0;
-    if (b == nb) cnt[b] = 0;
+    if (b > nb) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < b)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    offs[b] = (uint32_t)lo;
 }
 
-__global__ void k_seg_counts(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t* __restrict__ segcnt,
-                             uint32_t seg) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) segcnt[b] = (cnt[b] + seg - 1) / seg;
-    if (b == nb) segcnt[b] = 0;
+// One block: v[b] = f(b) for b < nb, v[nb] = 0; vals = v (optional), offs = exclusive prefix sums.
+// MODE 0 (partials of the affine level): f(b) = the seg-length thread ranges bucket b's references
+// [off[b], off[b + 1]) meet; MODE 1 (XYZZ level): f(b) = ceil(cnt[b] / seg).
+static constexpr int kScanThreads = 1024;
+template <int MODE>
+__global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restrict__ in, uint32_t nb, uint32_t seg,
+                                                        uint32_t* __restrict__ vals, uint32_t* __restrict__ offs) {
+    auto f = [&](uint32_t b) -> uint32_t {
+        if (b >= nb) return 0u;
+        if (MODE == 0) {
+            const uint32_t o = in[b], c = in[b + 1] - o;
+            return c ? (o + c - 1) / seg - o / seg + 1 : 0u;
+        }
+        return (in[b] + seg - 1) / seg;
+    };
+    const uint32_t per = (nb + 1 + kScanThreads - 1) / kScanThreads;
+    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb + 1);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += f(b);
+    using Scan = hipcub::BlockScan<uint32_t, kScanThreads>;
+    __shared__ typename Scan::TempStorage tmp;
+    uint32_t pre;
+    Scan(tmp).ExclusiveSum(sum, pre);
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t v = f(b);
+        if (vals) vals[b] = v;
+        offs[b] = pre;
+        pre += v;
+    }
 }
-
-
-__global__ void k_partial_counts(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, uint32_t nb,
-                                 uint32_t* __restrict__ np, uint32_t seg) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) np[b] = cnt[b] ? (off[b] + cnt[b] - 1) / seg - off[b] / seg + 1 : 0;
-    if (b == nb) np[b] = 0;
+void launch_scan_partials(const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np, uint32_t* np_off, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan1<0>, dim3(1), dim3(kScanThreads), 0, s, offs, nb, seg, np, np_off);
 }
-void launch_partial_counts(const uint32_t* off, const uint32_t* cnt, uint32_t nb, uint32_t* np, uint32_t seg,
-                           hipStream_t s) {
-    const int gb = (int)((nb + 1 + kLight - 1) / kLight);
-    hipLaunchKernelGGL(k_partial_counts, dim3(gb), dim3(kLight), 0, s, off, cnt, nb, np, seg);
-}
-
-void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s) {
-    const int gb = (int)((nb + 1 + kLight - 1) / kLight);
-    hipLaunchKernelGGL(k_seg_counts, dim3(gb), dim3(kLight), 0, s, cnt, nb, segcnt, seg);
+void launch_scan_segs(const uint32_t* cnt, uint32_t nb, uint32_t seg, uint32_t* segcnt, uint32_t* seg_off, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan1<1>, dim3(1), dim3(kScanThreads), 0, s, cnt, nb, seg, segcnt, seg_off);
 }
 
 uint32_t seg1_len(bool g2) {
@@ -214,118 +238,146 @@ void msm_ws_note_overflow(MsmWorkspace* ws) {
     if (ws) ws->cap_scale = std::min(ws->cap_scale * 1.5, 64.0);
 }
 
-void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
-    void* t = ws->cub.ensure(tb);
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
-}
-
 static double msm_cap_env() {  // SPX_MSM_CAP_SCALE (tests): scales the compacted-key capacity, e.g. 0.5 forces overflow
     const char* e = getenv("SPX_MSM_CAP_SCALE");
     const double v = e ? atof(e) : 1.0;
     return v > 0 ? v : 1.0;
 }
 
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s,
-                   const MsmShard& sh, uint32_t* status) {
-    MsmSorted o;
+MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_scale) {
+    MsmPlan o;
     const int G = std::max(1, sh.world);
     int g = 0;
     while ((1 << g) < G) ++g;
     if ((1 << g) != G || sh.rank < 0 || sh.rank >= G) throw std::runtime_error("MSM shard: bad rank / world");
-    const bool compact = G > 1 && !sh.dense;
-    std::vector<uint64_t> prefix;
-    uint64_t tot_sc = 0, tot_refs = 0;
+    o.compact = G > 1 && !sh.dense;
+    uint64_t tot_refs = 0;
     double split_refs = 0, whole_refs = 0;
     int nsplit = 0;
-    uint32_t nb = 0;
     for (int i = 0; i < ninst; ++i) {
         MsmInst I = ih[i];
-        if (!I.size || I.c < 3 || I.c > 24) {
-            if (!I.size) continue;  // empty MSM: infinity
-            throw std::runtime_error("MSM window bits out of range");
-        }
+        if (!I.size) continue;  // empty MSM: infinity
+        if (I.c < 3 || I.c > 24) throw std::runtime_error("MSM window bits out of range");
         const uint32_t lbf = I.c - 1;  // log2 of the instance's buckets
-        if (G > 1 && (int)lbf - g >= 2) {  // split by bucket range
+        if (G > 1 && (int)lbf - g >= 2) {  // split: buckets dealt round-robin over the ranks
             I.lb = lbf - g;
+            I.lg = (uint32_t)g;
             I.sel = (uint32_t)sh.rank;
             split_refs += (double)I.size * I.W / G;
             ++nsplit;
         } else if (i % G == sh.rank) {  // whole, on its owner
             I.lb = lbf;
+            I.lg = 0;
             I.sel = 0;
             whole_refs += (double)I.size * I.W;
         } else {
             continue;
         }
         I.out = (uint32_t)i;
-        I.bucket_off = nb;
+        I.bucket_off = o.nb;
         I.ref_off = (uint32_t)tot_refs;
-        nb += 1u << I.lb;
-        prefix.push_back(tot_sc);
-        tot_sc += I.size;
+        o.nb += 1u << I.lb;
+        o.prefix.push_back(o.tot_sc);
+        o.tot_sc += I.size;
         tot_refs += (uint64_t)I.size * I.W;
         o.mu_max = std::max(o.mu_max, (double)I.size * I.W / (double)(1u << lbf));
-        o.any_sel |= I.sel != 0;
+        o.any_split |= I.lg != 0;
         o.insts.push_back(I);
     }
     const int nact = (int)o.insts.size();
-    prefix.push_back(tot_sc);
+    o.prefix.push_back(o.tot_sc);
     if (tot_refs >= 0xffffffffull) throw std::runtime_error("MSM batch too large");
-    if (compact) {
-        // expected in-range digits plus a margin: ~8 standard deviations of the uniform case and a fixed
-        // slack per instance (the top window of a small-c instance crowds the low buckets)
-        const double cap = whole_refs + (split_refs + 8.0 * std::sqrt(split_refs) + 2048.0 * nsplit) * ws->cap_scale * msm_cap_env();
+    if (o.compact) {
+        // expected own digits plus a margin: ~8 standard deviations of the uniform case and a fixed
+        // slack per split instance
+        const double cap = whole_refs + (split_refs + 8.0 * std::sqrt(split_refs) + 2048.0 * nsplit) * cap_scale * msm_cap_env();
         tot_refs = std::min<uint64_t>(tot_refs, (uint64_t)std::ceil(cap));
     }
-    o.nb = nb;
     o.tot_refs = tot_refs;
-    if (!nact) return o;
-    o.d_insts = (MsmInst*)ws->insts.ensure(sizeof(MsmInst) * nact);
-    auto* d_prefix = (uint64_t*)ws->prefix.ensure(8 * (nact + 1));
-    HIPCHK(hipMemcpyAsync(o.d_insts, ws->pin.stage(o.insts.data(), nact), sizeof(MsmInst) * nact, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_prefix, ws->pin.stage(prefix.data(), nact + 1), 8 * (nact + 1), hipMemcpyHostToDevice, s));
-    o.counts = (uint32_t*)ws->counts.ensure(4 * (nb + 1));
+    // weighting tree: nodes after the chunked leaf level, 2^lb / 2^lgm per instance
+    o.node_off.resize(nact);
+    o.cnt.resize(nact);
+    uint32_t tot_nodes = 0;
+    for (int i = 0; i < nact; ++i) {
+        o.node_off[i] = tot_nodes;
+        const int lg = (int)o.insts[i].lb - (int)std::min<uint32_t>(kTreeChunkLog, o.insts[i].lb - 1);
+        o.cnt[i] = 1u << lg;
+        tot_nodes += o.cnt[i];
+        o.levels = std::max(o.levels, lg);
+    }
+    o.wp.assign((size_t)(o.levels + 1) * (nact + 1), 0);
+    o.cin.assign((size_t)(o.levels + 1) * nact, 0);
+    uint32_t maxc = 1;
+    for (int i = 0; i < nact; ++i) maxc = std::max(maxc, o.cnt[i]);
+    o.top_from = o.levels + 1;
+    for (int lv = 0; lv <= o.levels; ++lv) {
+        uint64_t acc = 0;
+        for (int i = 0; i < nact; ++i) {
+            uint32_t nin = lv == 0 ? (o.cnt[i] * 2) : std::max(1u, o.cnt[i] >> (lv - 1));
+            uint32_t nout = lv == 0 ? o.cnt[i] : std::max(1u, o.cnt[i] >> lv);
+            o.cin[(size_t)lv * nact + i] = nin;
+            o.wp[(size_t)lv * (nact + 1) + i] = acc;
+            acc += nout;
+        }
+        o.wp[(size_t)lv * (nact + 1) + nact] = acc;
+        if (lv >= 1 && o.top_from > o.levels && std::max(1u, maxc >> (lv - 1)) <= kTopNodes) o.top_from = lv;
+    }
+    return o;
+}
+
+void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
+    // [insts | prefix | wp | cin | node_off], 16-byte aligned parts, one pinned staging copy
+    const int nact = (int)p.insts.size();
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t b0 = al(sizeof(MsmInst) * nact), b1 = al(8 * p.prefix.size()), b2 = al(8 * p.wp.size()),
+                 b3 = al(4 * p.cin.size()), b4 = al(4 * p.node_off.size());
+    std::vector<uint8_t> h(b0 + b1 + b2 + b3 + b4, 0);
+    size_t o = 0;
+    memcpy(h.data() + o, p.insts.data(), sizeof(MsmInst) * nact), o += b0;
+    memcpy(h.data() + o, p.prefix.data(), 8 * p.prefix.size()), o += b1;
+    memcpy(h.data() + o, p.wp.data(), 8 * p.wp.size()), o += b2;
+    memcpy(h.data() + o, p.cin.data(), 4 * p.cin.size()), o += b3;
+    memcpy(h.data() + o, p.node_off.data(), 4 * p.node_off.size());
+    uint8_t* d = (uint8_t*)ws->tables.ensure(h.size());
+    // pinned staging: the copy may run after this returns; the arena is reset after a covering sync
+    HIPCHK(hipMemcpyAsync(d, ws->pin.stage(h.data(), h.size()), h.size(), hipMemcpyHostToDevice, s));
+    p.d_insts = (MsmInst*)d;
+    p.d_prefix = (uint64_t*)(d + b0);
+    p.d_wp = (uint64_t*)(d + b0 + b1);
+    p.d_cin = (uint32_t*)(d + b0 + b1 + b2);
+    p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
+}
+
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s) {
+    MsmSorted o;
+    const uint32_t nb = p.nb;
+    const uint64_t n = p.tot_refs;
+    const int nact = (int)p.insts.size();
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
-    uint32_t* cursor = (uint32_t*)ws->cursor.ensure(4 * (nb + 1));
-    o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(tot_refs, 1));
-    o.segcnt = (uint32_t*)ws->segcnt.ensure(4 * (nb + 1));
-    o.soa = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
-    o.sob = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
-    o.spare = cursor;
-    // (bucket, reference) pairs, LSD radix sort on the bucket bits, runs -> offsets and counts
-    const uint64_t n = tot_refs;
+    o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(n, 1));
+    // (bucket, reference) pairs, LSD radix sort on the bucket bits, bucket bounds by binary search
     int bits = 1;
     while ((1ull << bits) <= nb) ++bits;  // keys 0..nb; the compact filler ~0 has all these bits set
     uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * std::max<uint64_t>(n, 1));
     uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * std::max<uint64_t>(n, 1));
     uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
-    const int gsc = (int)((tot_sc + kLight - 1) / kLight);
+    const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
     kp_begin(KP_SORT, s);
-    if (compact) {
-        uint32_t* kc = (uint32_t*)ws->kcur.ensure(4);
-        HIPCHK(hipMemsetAsync(kc, 0, 4, s));
-        HIPCHK(hipMemsetAsync(ka, 0xff, 4 * n, s));
-        hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, nact, tot_sc, nb, scalars,
-                           ka, va, kc, (uint32_t)n, status);
-    } else {
-        hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, o.d_insts, d_prefix, nact, tot_sc, nb, scalars,
-                           ka, va, nullptr, 0u, nullptr);
-    }
+    if (p.compact)
+        hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
+                           scalars, ka, va, (uint32_t)n, st);
+    else
+        hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
+                           scalars, ka, va, 0u, st);
     hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
     size_t tb = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
     void* t = ws->cub.ensure(tb);
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
     o.refs = dv.Current();
-    HIPCHK(hipMemsetAsync(cursor, 0, 4 * (nb + 1), s));
-    hipLaunchKernelGGL(k_bucket_runs, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, dk.Current(), n, nb,
-                       o.offs, cursor);
-    hipLaunchKernelGGL(k_bucket_counts, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, o.offs, cursor, nb,
-                       o.counts);
-    exclusive_scan(ws, o.counts, o.offs, nb + 1, s);  // = run starts; empty buckets share the next offset
-    kp_end(32.0 * tot_sc + 4.0 * 8 * n, s);
+    hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, dk.Current(), n, nb,
+                       o.offs);
+    kp_end(32.0 * p.tot_sc + 4.0 * 8 * n, s);
     return o;
 }
 

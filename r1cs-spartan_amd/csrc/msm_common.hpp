@@ -24,6 +24,7 @@ static constexpr uint32_t kSeg = SPX_XYZZ_SEG;  // partials per thread, XYZZ acc
 #define SPX_TREE_CHUNK_LOG 2
 #endif
 static constexpr uint32_t kTreeChunkLog = SPX_TREE_CHUNK_LOG;  // buckets per running-sum chunk of the weighting leaf: 4
+static constexpr uint32_t kTopNodes = 16;  // k_tree_top: the levels whose input has <= 16 nodes, one launch
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
 
@@ -112,32 +113,49 @@ struct PinArena {
 };
 
 struct MsmWorkspace {
-    DBuf insts, prefix, counts, offs, cursor, refs, segcnt, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, tprefix,
-        keys_a, keys_b, vals_a, kcur;
+    DBuf tables, offs, refs, segcnt, spare, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a;
     // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
-    // bucket ranges (e.g. many equal values) stops overflowing after its first batch
+    // rank's buckets (e.g. many equal values) stops overflowing after its first batch
     double cap_scale = 1.0;
     PinArena pin;
 };
 
-void exclusive_scan(MsmWorkspace* ws, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
-
-// Result of the digit / sort stage of a batch (device pointers into the workspace).
-struct MsmSorted {
-    uint32_t nb = 0;          // local buckets in the batch (this rank's ranges)
-    uint64_t tot_refs = 0;    // key slots: upper bound of the (scalar, window) references with a digit in range
-    double mu_max = 0;        // largest expected references per bucket over the batch's instances
-    bool any_sel = false;     // some instance weights a bucket range that does not start at bucket 0
-    uint32_t *counts, *offs, *refs, *segcnt, *soa, *sob, *spare;
-    MsmInst* d_insts;
-    std::vector<MsmInst> insts;  // host copy of the active instances, driver fields filled in
+// Host plan of a batch: the instances this rank works on (driver fields filled in), the key slots,
+// the weighting tree's shape, and their device copy (ONE staged upload per batch).
+struct MsmPlan {
+    std::vector<MsmInst> insts;   // active instances
+    std::vector<uint64_t> prefix;  // scalar prefix over the active instances (nact + 1)
+    uint32_t nb = 0;              // local buckets in the batch
+    uint64_t tot_sc = 0;          // scalars digitised
+    uint64_t tot_refs = 0;        // key slots: upper bound of the references with a digit in range
+    bool compact = false;         // proof-sharded keys (only in-range digits, capacity tot_refs)
+    double mu_max = 0;            // largest expected references per bucket over the active instances
+    bool any_split = false;
+    // weighting tree: per instance, node offset and node count after the chunked leaf; levels above it
+    std::vector<uint32_t> node_off, cnt;
+    int levels = 0;     // tree levels above the leaf (max over instances)
+    int top_from = 1;   // first level done by k_tree_top (all levels >= it); levels below run one launch each
+    std::vector<uint64_t> wp;   // per level: work prefixes (levels + 1) x (nact + 1)
+    std::vector<uint32_t> cin;  // per level: input node counts (levels + 1) x nact
+    // device copies
+    MsmInst* d_insts = nullptr;
+    uint64_t *d_prefix = nullptr, *d_wp = nullptr;
+    uint32_t *d_cin = nullptr, *d_noff = nullptr;
 };
-// instances of `ih` this rank works on, keys of their in-range digits sorted by bucket
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmInst* ih, int ninst, const Fr* scalars, hipStream_t s,
-                   const MsmShard& sh, uint32_t* status);
-// partials of the load-balanced affine level per bucket: the seg-length thread ranges its references meet
-void launch_partial_counts(const uint32_t* off, const uint32_t* cnt, uint32_t nb, uint32_t* np, uint32_t seg,
-                           hipStream_t s);
-void launch_seg_counts(const uint32_t* cnt, uint32_t nb, uint32_t* segcnt, uint32_t seg, hipStream_t s);
+MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_scale);
+void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s);
+
+// status words after a batch's outputs (zeroed with them): [0] status bits, [1] compacted-key
+// cursor, [2] keys-kernel ticket
+// Digit / sort stage: sorted (bucket, reference) pairs, per-bucket offsets (offs[nb] = references).
+struct MsmSorted {
+    uint32_t *offs, *refs;
+};
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* status_words, hipStream_t s);
+// partials of the load-balanced affine level per bucket (the seg-length thread ranges its references
+// meet) and their exclusive offsets, in one launch
+void launch_scan_partials(const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np, uint32_t* np_off, hipStream_t s);
+// next XYZZ level: segments of `seg` partials per bucket and their exclusive offsets, in one launch
+void launch_scan_segs(const uint32_t* cnt, uint32_t nb, uint32_t seg, uint32_t* segcnt, uint32_t* seg_off, hipStream_t s);
 
 }  // namespace spx

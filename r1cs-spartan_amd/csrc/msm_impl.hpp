@@ -468,7 +468,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
         A::st(So + base + k, a);
     } else {
         A::ld(a, Di + base + 2 * k);
-        if (has_r) {  // a lone root passes through: D stays (its buckets) x S for k_tree_offset
+        if (has_r) {  // a lone root passes through (its D is never read again)
             A::ld(b, Di + base + 2 * k + 1);
             tree_add<F>(a, b);
             tree_dbl<F>(a);
@@ -477,45 +477,93 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
     }
 }
 
-// A rank weighting bucket range sel (buckets [sel 2^lb, (sel + 1) 2^lb) of the instance) computed
-// sum_m (m + 1) X_m over local indices; the global weights add sel 2^lb S = sel D (D of the root).
+// The top levels of every instance's weighting tree in ONE launch: one workgroup per instance, its
+// nodes in LDS (the levels whose input has <= kTopNodes nodes; each is 2 dependent additions, so
+// launching them one by one cost a launch gap per level). Then, for an instance split over the ranks
+// (this rank holds buckets u = sel + G k, G = 2^lg, as local buckets k, and the tree computed
+// F = sum_k (k + 1) X_k, S = sum_k X_k), the rank's share sum_k (sel + G k + 1) X_k = G F - (G - 1 - sel) S;
+// finally the R = 2^384 Montgomery output for the host.
+static constexpr int kTopThreads = 128;
 template <class F>
-__global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_offset(const MsmInst* __restrict__ insts, int ninst,
-                                                                        const uint32_t* __restrict__ node_off,
-                                                                        Xyzz<F>* __restrict__ Fi,
-                                                                        const Xyzz<F>* __restrict__ Di) {
+__global__ __launch_bounds__(kTopThreads, 1) void k_tree_top(const MsmInst* __restrict__ insts, int nact,
+                                                             const uint32_t* __restrict__ node_off,
+                                                             const uint32_t* __restrict__ cin_top, int lv0, int levels,
+                                                             const Xyzz<F>* __restrict__ Fi, const Xyzz<F>* __restrict__ Si,
+                                                             const Xyzz<F>* __restrict__ Di, Xyzz<F>* __restrict__ out) {
     using A = Acc<F>;
-    const uint64_t t = tree_elem<F>();
-    if (t >= (uint64_t)ninst) return;
-    const uint32_t sel = insts[t].sel;
-    if (!sel) return;
-    const uint32_t o = node_off[t];
-    X29<typename A::T> d, acc, f;
-    A::ld(d, Di + o);
-    acc = d;
-#pragma unroll 1
-    for (int b = 30 - __clz(sel); b >= 0; --b) {  // sel d, double-and-add below the top bit
-        tree_dbl<F>(acc);
-        if ((sel >> b) & 1u) tree_add<F>(acc, d);
+    using T = typename A::T;
+    using O = Ops29<T>;
+    constexpr int kL = TreeLanes<F>::v;
+    __shared__ Xyzz<F> buf[2][3][kTopNodes];
+    const int i = blockIdx.x;
+    const MsmInst I = insts[i];
+    const uint32_t base = node_off[i];
+    const int grp = threadIdx.x / kL, ngrp = kTopThreads / kL;
+    // the instance's node count after the leaf: its input at lv0 is max(1, cnt >> (lv0 - 1))
+    uint32_t nin = cin_top[i];
+    for (uint32_t t = threadIdx.x; t < 3 * nin; t += blockDim.x) {
+        const uint32_t comp = t / nin, k = t % nin;
+        const Xyzz<F>* src = comp == 0 ? Fi : (comp == 1 ? Si : Di);
+        buf[0][comp][k] = src[base + k];
     }
-    A::ld(f, Fi + o);
-    tree_add<F>(f, acc);
-    A::st(Fi + o, f);
-}
-
-template <class F>
-__global__ void k_tree_out(const MsmInst* __restrict__ insts, int ninst, const uint32_t* __restrict__ node_off,
-                           const Xyzz<F>* __restrict__ Fi, Xyzz<F>* __restrict__ out) {
-    using T = typename R29<F>::T;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < ninst) {  // back to the R = 2^384 Montgomery domain, canonical, for the host
-        X29<T> a, b;
-        ld29<F>(a, Fi + node_off[i]);
+    __syncthreads();
+    int cur = 0;
+    for (int lv = lv0; lv <= levels; ++lv) {
+        const uint32_t nout = nin > 1 ? nin / 2 : 1;
+        for (uint32_t task = grp; task < 3 * nout; task += ngrp) {
+            const uint32_t comp = task / nout, k = task % nout;
+            const bool has_r = 2 * k + 1 < nin;
+            X29<T> a, b;
+            A::ld(a, &buf[cur][comp][2 * k]);
+            if (comp == 0) {  // F_l + D_r + F_r
+                if (has_r) {
+                    A::ld(b, &buf[cur][2][2 * k + 1]);
+                    tree_add<F>(a, b);
+                    A::ld(b, &buf[cur][0][2 * k + 1]);
+                    tree_add<F>(a, b);
+                }
+            } else if (has_r) {  // S_l + S_r; 2 (D_l + D_r)
+                A::ld(b, &buf[cur][comp][2 * k + 1]);
+                tree_add<F>(a, b);
+                if (comp == 2) tree_dbl<F>(a);
+            }
+            A::st(&buf[cur ^ 1][comp][k], a);
+        }
+        __syncthreads();
+        cur ^= 1;
+        nin = nout;
+    }
+    if (I.lg && grp == 0) {  // the rank's share of a split instance: G F - (G - 1 - sel) S
+        X29<T> f, sv, acc;
+        A::ld(f, &buf[cur][0][0]);
+#pragma unroll 1
+        for (uint32_t d = 0; d < I.lg; ++d) tree_dbl<F>(f);
+        const uint32_t k = (1u << I.lg) - 1 - I.sel;
+        if (k) {
+            A::ld(sv, &buf[cur][1][0]);
+            acc = sv;
+#pragma unroll 1
+            for (int b = 30 - __clz(k); b >= 0; --b) {  // k S, double-and-add below the top bit
+                tree_dbl<F>(acc);
+                if ((k >> b) & 1u) tree_add<F>(acc, sv);
+            }
+            T z;
+            O::zero(z);
+            O::template sub<2>(acc.y, z, acc.y);  // -(k S): y < 2p -> 2p - y < 2p
+            tree_add<F>(f, acc);
+        }
+        A::st(&buf[cur][0][0], f);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // back to the R = 2^384 Montgomery domain, canonical, for the host
+        using T1 = typename R29<F>::T;
+        X29<T1> a, b;
+        ld29<F>(a, &buf[cur][0][0]);
         f29_map(b.x, a.x, Q29::TO_R1);
         f29_map(b.y, a.y, Q29::TO_R1);
         f29_map(b.zz, a.zz, Q29::TO_R1);
         f29_map(b.zzz, a.zzz, Q29::TO_R1);
-        st29<F>(out + insts[i].out, b);
+        st29<F>(out + I.out, b);
     }
 }
 
@@ -525,43 +573,43 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     if (ninst <= 0) return;
     const bool g2 = sizeof(F) == sizeof(Fq2);
     const size_t psz = sizeof(Xyzz<F>);
-    // every output starts at infinity (all zero) and the status word at 0
+    // every output starts at infinity (all zero), the status words at 0
     HIPCHK(hipMemsetAsync(out_dev, 0, msm_out_bytes(g2, ninst), s));
-    uint32_t* status = (uint32_t*)((uint8_t*)out_dev + psz * ninst);
-    MsmSorted so = msm_sort(ws, ih, ninst, scalars, s, sh, status);
-    const int nact = (int)so.insts.size();
+    uint32_t* st = (uint32_t*)((uint8_t*)out_dev + psz * ninst);
+    MsmPlan pl = msm_plan(ih, ninst, sh, ws->cap_scale);
+    const int nact = (int)pl.insts.size();
     if (!nact) return;
-    const uint32_t nb = so.nb;
-    const uint64_t tot_refs = so.tot_refs;
+    msm_upload_plan(ws, pl, s);
+    MsmSorted so = msm_sort(ws, pl, scalars, st, s);
+    const uint32_t nb = pl.nb;
+    const uint64_t tot_refs = pl.tot_refs;
     // level 1: affine references -> XYZZ partials, one per segment of kSeg1 references
     const uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
-    launch_partial_counts(so.offs, so.counts, nb, so.segcnt, kSeg1, s);
-    exclusive_scan(ws, so.segcnt, so.soa, nb + 1, s);
+    uint32_t* cur_cnt = (uint32_t*)ws->segcnt.ensure(4 * (nb + 1));
+    uint32_t* spare_cnt = (uint32_t*)ws->spare.ensure(4 * (nb + 1));
+    uint32_t* cur_off = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
+    uint32_t* nxt_off = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
+    launch_scan_partials(so.offs, nb, kSeg1, cur_cnt, cur_off, s);
     const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
-    hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, so.soa, so.refs, pts, PA,
+    hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, cur_off, so.refs, pts, PA,
                        kSeg1);
     // algorithmic bytes: every reference (4 B) and its affine point once (96 / 192 B, not the slot's
     // padding), one XYZZ partial per segment
     kp_end((double)tot_refs * (4.0 + sizeof(Aff<F>)) + (double)(tot_refs / kSeg1) * psz, s, (double)tot_refs);
-    uint32_t* cur_cnt = so.segcnt;
-    uint32_t* cur_off = so.soa;
-    uint32_t* nxt_off = so.sob;
-    uint32_t* spare_cnt = so.spare;
     Xyzz<F>* cur = PA;
     Xyzz<F>* nxt = PB;
     uint64_t cur_max_segs = max_segs;
     // XYZZ partial levels, planned from the expected occupancy (no host round trip): a bucket with
     // mu references on average rarely exceeds mu + 6 sqrt(mu) + 16; the weighting leaf adds the
     // partials of any bucket that does (k_tree_chunk), so the plan decides speed, never correctness
-    const double mu = so.mu_max;
+    const double mu = pl.mu_max;
     uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1;  // partials per bucket
     while (m > 1) {
-        launch_seg_counts(cur_cnt, nb, spare_cnt, kSeg, s);
-        exclusive_scan(ws, spare_cnt, nxt_off, nb + 1, s);
+        launch_scan_segs(cur_cnt, nb, kSeg, spare_cnt, nxt_off, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
         hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur_cnt,
@@ -573,62 +621,28 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
         cur_max_segs = nsegs;
         m = (m + kSeg - 1) / kSeg;
     }
-    // bucket weighting tree over each instance's 2^lb local buckets
-    std::vector<uint32_t> node_off(nact), cnt(nact);
+    // bucket weighting tree over each instance's 2^lb local buckets: leaf, middle levels, top
     uint32_t tot_nodes = 0;
-    int levels = 0;
-    for (int i = 0; i < nact; ++i) {
-        node_off[i] = tot_nodes;
-        // nodes after the chunked leaf level: 2^lb / 2^lgm (lb >= 2, lgm = min(kTreeChunkLog, lb - 1))
-        const int lg = (int)so.insts[i].lb - (int)std::min<uint32_t>(kTreeChunkLog, so.insts[i].lb - 1);
-        cnt[i] = 1u << lg;
-        tot_nodes += cnt[i];
-        levels = std::max(levels, lg);
-    }
-    // per-level work prefixes: 3 threads per output node; per-level input node counts
-    std::vector<uint64_t> wp((size_t)(levels + 1) * (nact + 1));
-    std::vector<uint32_t> cin((size_t)(levels + 1) * nact);
-    for (int lv = 0; lv <= levels; ++lv) {
-        uint64_t acc = 0;
-        for (int i = 0; i < nact; ++i) {
-            uint32_t nin = lv == 0 ? (cnt[i] * 2) : std::max(1u, cnt[i] >> (lv - 1));
-            uint32_t nout = lv == 0 ? cnt[i] : std::max(1u, cnt[i] >> lv);
-            cin[(size_t)lv * nact + i] = nin;
-            wp[(size_t)lv * (nact + 1) + i] = acc;
-            acc += nout;
-        }
-        wp[(size_t)lv * (nact + 1) + nact] = acc;
-    }
-    const size_t tbytes = 8 * wp.size() + 4 * cin.size() + 4 * node_off.size();
-    auto* tp = (uint8_t*)ws->tprefix.ensure(tbytes);
-    uint64_t* d_wp = (uint64_t*)tp;
-    uint32_t* d_cin = (uint32_t*)(tp + 8 * wp.size());
-    uint32_t* d_noff = d_cin + cin.size();
-    // pinned staging: this function returns before the copies run (no sync), the vectors do not outlive it
-    HIPCHK(hipMemcpyAsync(d_wp, ws->pin.stage(wp.data(), wp.size()), 8 * wp.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_cin, ws->pin.stage(cin.data(), cin.size()), 4 * cin.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_noff, ws->pin.stage(node_off.data(), node_off.size()), 4 * node_off.size(),
-                          hipMemcpyHostToDevice, s));
+    for (int i = 0; i < nact; ++i) tot_nodes += pl.cnt[i];
     auto* TA = (Xyzz<F>*)ws->tree_a.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
     auto* TB = (Xyzz<F>*)ws->tree_b.ensure(3 * psz * std::max<uint32_t>(tot_nodes, 1));
     Xyzz<F>* A3[3] = {TA, TA + tot_nodes, TA + 2 * (size_t)tot_nodes};
     Xyzz<F>* B3[3] = {TB, TB + tot_nodes, TB + 2 * (size_t)tot_nodes};
     kp_begin(g2 ? KP_RED_G2 : KP_RED_G1, s);
     {
-        uint64_t work = wp[nact];
-        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, so.d_insts, d_wp, nact, d_noff,
-                           cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
+        uint64_t work = pl.wp[nact];
+        hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, pl.d_insts, pl.d_wp, nact,
+                           pl.d_noff, cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
     }
-    for (int lv = 1; lv <= levels; ++lv) {
-        uint64_t work = 3 * wp[(size_t)lv * (nact + 1) + nact];
-        hipLaunchKernelGGL(k_tree_level<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, d_wp + (size_t)lv * (nact + 1),
-                           nact, d_noff, d_cin + (size_t)lv * nact, A3[0], A3[1], A3[2], B3[0], B3[1], B3[2]);
+    for (int lv = 1; lv < pl.top_from; ++lv) {
+        uint64_t work = 3 * pl.wp[(size_t)lv * (nact + 1) + nact];
+        hipLaunchKernelGGL(k_tree_level<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s,
+                           pl.d_wp + (size_t)lv * (nact + 1), nact, pl.d_noff, pl.d_cin + (size_t)lv * nact, A3[0], A3[1],
+                           A3[2], B3[0], B3[1], B3[2]);
         std::swap(A3, B3);
     }
-    if (so.any_sel)
-        hipLaunchKernelGGL(k_tree_offset<F>, dim3(tree_blocks<F>((uint64_t)nact)), dim3(kHeavy), 0, s, so.d_insts, nact,
-                           d_noff, A3[0], A3[2]);
-    hipLaunchKernelGGL(k_tree_out<F>, dim3((nact + 63) / 64), dim3(64), 0, s, so.d_insts, nact, d_noff, A3[0],
+    hipLaunchKernelGGL(k_tree_top<F>, dim3(nact), dim3(kTopThreads), 0, s, pl.d_insts, nact, pl.d_noff,
+                       pl.d_cin + (size_t)pl.top_from * nact, pl.top_from, pl.levels, A3[0], A3[1], A3[2],
                        (Xyzz<F>*)out_dev);
     kp_end((double)nb * psz, s);
     HIPCHK(hipGetLastError());

@@ -38,6 +38,9 @@ Ctx::Ctx(int dev) : device(dev) {
     SPX_HIP(hipSetDevice(dev));
     SPX_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     SPX_HIP(hipHostMalloc((void**)&pin, kPinBytes));
+    SPX_HIP(hipHostGetDevicePointer((void**)&pin_dev_base, pin, 0));
+    SPX_HIP(hipMalloc((void**)&ticket, 64));
+    SPX_HIP(hipMemset(ticket, 0, 64));
     msm = msm_ws_create();
     comm.reset(new LocalComm());
 }
@@ -54,6 +57,7 @@ Ctx::~Ctx() {
     if (side) (void)hipStreamDestroy(side);
     msm_ws_destroy(msm);
     scratch.release();
+    if (ticket) (void)hipFree(ticket);
     if (pin) (void)hipHostFree(pin);
     if (stream) (void)hipStreamDestroy(stream);
 }
@@ -571,6 +575,11 @@ static HFr ld_hfr(const uint8_t* p) {  // device Montgomery bytes -> host Fr
     memcpy(r.v, p, 32);
     return r;
 }
+static Fr dev_fr(const HFr& x) {  // host Fr -> device Fr (same Montgomery bytes), e.g. a kernel argument
+    Fr r;
+    memcpy(&r, x.v, 32);
+    return r;
+}
 static HFr eq1(const HFr& tau, const HFr& t) {  // eq(tau, t) = 1 - tau - t + 2 tau t  (eq.rs:14)
     HFr tt = tau * t;
     return HFr::one() - tau - t + tt + tt;
@@ -679,6 +688,7 @@ static Affine<HFq> commit_finish(Ctx& C, PP& P, const Fr* z, uint64_t n, Comm& c
     const uint8_t* h = C.pin_at(Ctx::kPinCommit, msm_out_bytes(false, 1), 4 << 10);
     if (msm_status(h, false, 1) & kMsmOverflow) {  // compacted keys overflowed: once more with a slot per digit
         msm_ws_note_overflow(C.msm);
+        ++C.msm_reruns;
         MsmShard sh = shard_of(comm);
         sh.dense = true;
         commit_launch(C, P, z, n, sh);
@@ -710,7 +720,7 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z, int L, const MsmShard& sh, b
         g_kprof = nullptr;
     }
     Fr* q = C.buf<Fr>(Ctx::kSlotLvl0Q, 32 * half);
-    launch_open_level(z, nullptr, q, nullptr, half, st);
+    launch_open_level(z, nullptr, q, Fr{}, half, st);
     MsmInst I{};
     I.pts_off = P.g2_off[0];
     I.stride = (uint32_t)half;
@@ -731,6 +741,7 @@ static Affine<HFq2> lvl0_finish(Ctx& C, PP& P, const Fr* z, int L, Comm& comm, b
     const uint8_t* h = C.pin_at(Ctx::kPinLvl0, msm_out_bytes(true, 1), 4 << 10);
     if (msm_status(h, true, 1) & kMsmOverflow) {
         msm_ws_note_overflow(on_side ? C.msm_side : C.msm);
+        ++C.msm_reruns;
         MsmShard sh = shard_of(comm);
         sh.dense = true;
         lvl0_launch(C, P, z, L, sh, on_side);
@@ -758,20 +769,16 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
     OpenOut res;
     res.proofs.resize(L);
     if (proof0) res.proofs[0] = *proof0;
-    Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
     Fr* q = C.buf<Fr>(Ctx::kSlotOpenQ, 32 * n);
     Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(n / 2, 1)),
                    C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(n / 4, 1))};
-    uint8_t* ps = C.pin_at(Ctx::kPinStage, 32 * L, 64 << 10);
-    memcpy(ps, point.data(), 32 * L);
-    SPX_HIP(hipMemcpyAsync(pt, ps, 32 * L, hipMemcpyHostToDevice, C.stream));
     std::vector<MsmInst> insts(L - first);
     const Fr* rin = z;
     uint64_t qoff = 0;
     for (int i = 0; i < L; ++i) {
         const uint64_t half = n >> (i + 1);
         Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, q + qoff, pt + i, half, C.stream);
+        launch_open_level(rin, rout, q + qoff, dev_fr(point[i]), half, C.stream);
         rin = rout;
         if (i < first) continue;  // fold only; the level's proof is proof0 (its quotient is overwritten next)
         MsmInst& I = insts[i - first];
@@ -798,6 +805,7 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
         C.sync();
         if (!nm || !(msm_status(h, true, nm) & kMsmOverflow)) break;
         msm_ws_note_overflow(C.msm);  // compacted keys overflowed: once more with a slot per digit
+        ++C.msm_reruns;
     }
     res.eval = ld_hfr(h + ob);
     std::vector<Affine<HFq2>> part = msm_results<HFq2>(comm, h, nm);
@@ -814,16 +822,13 @@ static OpenOut open_stub(Ctx& C, const Fr* z_local, int L, const std::vector<HFr
     const int nloc = L - g;
     OpenOut res;
     res.proofs.assign(L, Affine<HFq2>{HFq2::zero(), HFq2::zero(), true});
-    Fr* pt = C.buf<Fr>(Ctx::kSlotOpenPt, 32 * L);
     Fr* bufs[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
                    C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
     uint8_t* h = C.pin_at(Ctx::kPinOpen, 32 * (L + 1), 56 << 10);
-    memcpy(h, point.data(), 32 * L);
-    SPX_HIP(hipMemcpyAsync(pt, h, 32 * L, hipMemcpyHostToDevice, C.stream));
     const Fr* rin = z_local;
     for (int i = 0; i < nloc; ++i) {
         Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, nullptr, pt + i, nl >> (i + 1), C.stream);
+        launch_open_level(rin, rout, nullptr, dev_fr(point[i]), nl >> (i + 1), C.stream);
         rin = rout;
     }
     SPX_HIP(hipMemcpyAsync(h + 32 * L, rin, 32, hipMemcpyDeviceToHost, C.stream));
@@ -922,7 +927,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Fr *Z1 = take(n2), *Z2 = take(n4);
     Fr* partial = take(std::max<uint64_t>(3 * 2048, std::max(I.rows.nchunks, I.cols.nchunks)));
     Fr *eqlo = take(8192), *eqhi = take(8192);
-    Fr* res3 = take(64);
     Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
     uint8_t* hp = C.pin_at(Ctx::kPinHp, 1 << 16, 64 << 10);
 
@@ -1025,7 +1029,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     proof.u64((uint64_t)L);
     std::vector<HFr> r_x;
     HFr Cc = HFr::one();
-    Fr* rdev = chdev + L;  // challenges r_1.. on device
+    Fr* res_dev = C.pin_dev<Fr>(hp);  // the rounds' sums land in pinned host memory (hp)
     Tables3 cur{{Az, Bz, Cz}};
     const Fr* Ecur = E1;
     Fr* Ebuf[2] = {Ea, Eb};
@@ -1039,8 +1043,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             out = Tables3{{fb[0], fb[1], fb[2]}};
             if (i < L - g) Eout = Ebuf[i & 1];
         }
-        launch_sc1_round(fold, cur, out, Ecur, Eout, fold ? rdev + (i - 2) : nullptr, half, partial, res3, C.stream);
-        SPX_HIP(hipMemcpyAsync(hp, res3, 96, hipMemcpyDeviceToHost, C.stream));
+        launch_sc1_round(fold, cur, out, Ecur, Eout, fold ? dev_fr(r_x[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
+                         C.stream);
         C.sync();
         HFr gs[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1057,8 +1061,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         HFr ch = T.rand_fr();
         r_x.push_back(ch);
         Cc = Cc * eq1(tau[i - 1], ch);
-        memcpy(hp + 128, &ch, 32);
-        SPX_HIP(hipMemcpyAsync(rdev + (i - 1), hp + 128, 32, hipMemcpyHostToDevice, C.stream));
         if (fold) {
             cur = out;
             if (Eout) Ecur = Eout;
@@ -1152,7 +1154,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // ---- sumcheck #2 (lib.rs:114-131)
     proof.u64((uint64_t)L);
     std::vector<HFr> r_y;
-    Fr* r2dev = chdev + 3 * L + 3;
     const Fr* Mc = M0;
     const Fr* Zc = zl;
     Fr* Mb[2] = {M1, M2};
@@ -1162,8 +1163,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         const bool fold = i >= 2;
         Fr* Mo = fold ? Mb[i & 1] : nullptr;
         Fr* Zo = fold ? Zb[i & 1] : nullptr;
-        launch_sc2_round(fold, Mc, Zc, Mo, Zo, fold ? r2dev + (i - 2) : nullptr, half, partial, res3, C.stream);
-        SPX_HIP(hipMemcpyAsync(hp, res3, 96, hipMemcpyDeviceToHost, C.stream));
+        launch_sc2_round(fold, Mc, Zc, Mo, Zo, fold ? dev_fr(r_y[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
+                         C.stream);
         C.sync();
         HFr ps[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1178,8 +1179,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
         HFr ch = T.rand_fr();
         r_y.push_back(ch);
-        memcpy(hp + 128, &ch, 32);
-        SPX_HIP(hipMemcpyAsync(r2dev + (i - 1), hp + 128, 32, hipMemcpyHostToDevice, C.stream));
         if (fold) {
             Mc = Mo;
             Zc = Zo;
@@ -1437,7 +1436,7 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
     for (int i = 0; i < L; ++i) {
         const uint64_t half = n >> (i + 1);
         Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, EQ, ch + L + 3 + i, half, C.stream);
+        launch_open_level(rin, rout, EQ, dev_fr(r_y[i]), half, C.stream);
         rin = rout;
     }
     uint8_t* hp = C.pin_at(Ctx::kPinOpen, 32, 56 << 10);

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -78,6 +79,18 @@ struct LocalComm : Comm {
     int size() const override { return 1; }
     void allgather(const void* s, void* r, size_t b) override { memcpy(r, s, b); }
 };
+// Rehearsal of ONE rank of a proof-sharded prove on a GPU of its own (bench / scaling estimates):
+// every allgather returns this rank's contribution in all `world` slots, so the rank does exactly a
+// real rank's device and host work without its peers. The proofs it outputs are NOT valid proofs.
+struct SoloComm : Comm {
+    int r, w;
+    SoloComm(int rank, int world) : r(rank), w(world) {}
+    int rank() const override { return r; }
+    int size() const override { return w; }
+    void allgather(const void* s, void* rv, size_t b) override {
+        for (int k = 0; k < w; ++k) memcpy((uint8_t*)rv + k * b, s, b);
+    }
+};
 struct GroupState {
     int world;
     std::mutex mu;
@@ -141,10 +154,16 @@ struct Ctx {
         kPinBytes = 192 << 10
     };
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev_base = nullptr;  // the carve-out's device address (kernels write round results there)
+    template <class T>
+    T* pin_dev(const uint8_t* host_ptr) const {
+        return reinterpret_cast<T*>(pin_dev_base + (host_ptr - pin));
+    }
+    uint32_t* ticket = nullptr;  // device counter of the one-launch sumcheck rounds (0 between launches)
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
-    enum { kSlotCommit, kSlotOpenPt, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
+    enum { kSlotCommit, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
     DevMem slot[kSlots];
     template <class T = void>
     T* buf(int id, size_t bytes) {
@@ -154,6 +173,7 @@ struct Ctx {
     std::vector<std::pair<std::string, double>> timings;
     KProf kprof;
     uint64_t prove_seq = 0;  // proofs started on this context (identical on every rank of its communicator)
+    std::atomic<uint64_t> msm_reruns{0};  // MSM batches rerun dense after a compacted-key overflow
     Ctx(int dev);
     ~Ctx();
     // region [off, off + bytes) of the pinned carve-out (throws if it does not fit its region)

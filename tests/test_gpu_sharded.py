@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
     group = spx.CommGroup(G)
     out = [None] * G
+    reruns = [0] * G
     errs = []
     w = inst.w_bytes if w_bytes is None else w_bytes
 
@@ -25,6 +26,7 @@ def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
             mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
             pk = spx.MLArgumentForR1CS.index(ctx, *mats)
             out[r] = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, w, pp)
+            reruns[r] = ctx.msm_reruns()
         except Exception as e:  # surfaced below
             errs.append(repr(e))
 
@@ -34,7 +36,7 @@ def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
     for t in ths:
         t.join(timeout=600)
     assert not errs, errs
-    return out
+    return out, sum(reruns)
 
 
 @pytest.mark.parametrize("G,kind,log_n", [(2, 0, 6), (4, 0, 8), (8, 2, 9), (2, 1, 10), (8, 0, 12)])
@@ -44,9 +46,10 @@ def test_virtual_ranks_equal_single(spx, oc, G, kind, log_n):
     inst = oc.Instance(kind, log_n, log_v, 300 + log_n, param)
     ppb = oc.PP.keygen(log_n, 400 + log_n).serialize()
     want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
-    out = _prove_ranks(spx, G, inst, ppb)
+    out, reruns = _prove_ranks(spx, G, inst, ppb)
     for r in range(G):
         assert out[r] == want, "rank %d proof differs" % r
+    assert reruns == 0, "uniform scalars overflowed the planned key capacity"
 
 
 def test_virtual_ranks_forced_key_overflow(spx, oc):
@@ -58,22 +61,30 @@ def test_virtual_ranks_forced_key_overflow(spx, oc):
     want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
     os.environ["SPX_MSM_CAP_SCALE"] = "0.5"
     try:
-        out = _prove_ranks(spx, G, inst, ppb)
+        out, reruns = _prove_ranks(spx, G, inst, ppb)
     finally:
         del os.environ["SPX_MSM_CAP_SCALE"]
     assert all(p == want for p in out)
+    assert reruns > 0, "the halved capacity did not overflow"
 
 
-@pytest.mark.parametrize("fill", [1, 0])
+# every 7-bit window digit of this scalar is 1: at 2^9 (commitment window c = 7) all of a
+# commitment's digits land in bucket 0, i.e. on rank 0
+_ONES7 = sum(1 << (7 * w) for w in range(37))
+
+
+@pytest.mark.parametrize("fill", [_ONES7, 1, 0])
 def test_virtual_ranks_crowded_buckets(spx, oc, fill):
-    """a witness of equal values: every commitment digit lands in one bucket (one rank's range:
-    its compacted keys overflow and the batch is rerun dense), every opening quotient is 0. The
-    proof is not a valid one (the witness does not satisfy the matrices); it must still equal the
-    oracle's byte for byte."""
+    """a witness of equal values: every commitment digit of a window lands in one bucket (for
+    _ONES7 all of them on rank 0: its compacted keys overflow and the batch is rerun dense), every
+    opening quotient is 0. The proof is not a valid one (the witness does not satisfy the matrices);
+    it must still equal the oracle's byte for byte."""
     log_n, log_v, G = 9, 3, 4
     inst = oc.Instance(0, log_n, log_v, 950 + log_n, 0)
     ppb = oc.PP.keygen(log_n, 951).serialize()
     w = fill.to_bytes(32, "little") * ((1 << log_n) - (1 << log_v))
     want = oc.prove(inst.mats, inst.v_bytes, w, oc.PP.load(ppb), 0, 0)
-    out = _prove_ranks(spx, G, inst, ppb, w)
+    out, reruns = _prove_ranks(spx, G, inst, ppb, w)
     assert all(p == want for p in out)
+    if fill == _ONES7:
+        assert reruns > 0, "crowded scalars did not overflow rank 0's keys"

@@ -1,6 +1,9 @@
 """GPU busy summary from a rocprofv3 --kernel-trace CSV: wall span, time with >= 1 kernel running,
 and an estimate of SIMD occupancy (waves resident / 1024 SIMDs, one wave per SIMD for the
-register-heavy curve kernels) per kernel family. Usage: trace_busy.py <kernel_trace.csv> [t0_frac t1_frac]"""
+register-heavy curve kernels) per kernel family. Usage: trace_busy.py <kernel_trace.csv> [t0_frac t1_frac]
+Environment: TRACE_AFTER=<name> starts the window at the first kernel whose name contains it (e.g.
+k_sc1_round: skips setup); TRACE_TOP=<k> rows (default 20)."""
+import os
 import csv
 import re
 import sys
@@ -16,6 +19,10 @@ for r in rows:
     wg = int(r.get("Workgroup_Size") or r.get("Workgroup_Size_X") or 64)
     ev.append((s, e, r["Kernel_Name"], grid, wg))
 ev.sort()
+after = os.environ.get("TRACE_AFTER")
+if after:
+    first = next(s for s, e, name, *_ in ev if after in name)
+    ev = [x for x in ev if x[0] >= first]
 T0, T1 = ev[0][0], max(e for _, e, *_ in ev)
 lo, hi = T0 + f0 * (T1 - T0), T0 + f1 * (T1 - T0)
 ev = [x for x in ev if x[0] >= lo and x[1] <= hi]
@@ -42,7 +49,7 @@ for s, e, name, grid, wg in ev:
 print("span %.1f ms, >=1 kernel running %.1f%%, kernels %d" % (span / 1e6, 100 * busy / span, len(ev)))
 tot_occ = sum(v[1] for v in fam.values())
 print("SIMD-occupancy estimate (sum min(waves,1024) x duration / 1024 x span): %.1f%%" % (100 * tot_occ / (1024 * span)))
-for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])[:20]:
+for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])[: int(os.environ.get("TRACE_TOP", "20"))]:
     print("%-60s calls %6d  dur %9.1f ms  simd-share %5.1f%%" % (k, v[2], v[0] / 1e6, 100 * v[1] / (1024 * span)))
 # timeline: occupancy estimate per 1/40 of the span (phases of the bench show up as plateaus)
 nb = 40

@@ -1,0 +1,95 @@
+"""Proof-sharded throughput with G VIRTUAL ranks in ONE process on one GPU (in-process communicator,
+one thread per rank, B contexts per rank): the same prover code as bench.py --shard proof at N = G,
+without multi-process GPU sharing, so rocprofv3 can trace it (one process) and its counters divide
+the whole job's work by rank.
+
+usage: python tools/vrank_bench.py --G 4 [--log-n 20] [--inflight 4] [--proofs 64] [--cached] [--steps 1]
+Prints one JSON line: constraints/s, ms per proof, and the proofs' equality with rank 0's."""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--G", type=int, default=4)
+    ap.add_argument("--log-n", type=int, default=20)
+    ap.add_argument("--log-v", type=int, default=5)
+    ap.add_argument("--inflight", type=int, default=4, help="contexts (proofs in flight) per rank")
+    ap.add_argument("--proofs", type=int, default=64, help="proofs per step")
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cached", action="store_true", help="index-cached matrix transcript")
+    ap.add_argument("--solo", action="store_true",
+                    help="rehearsal: only rank 0 of the G, without peers (spx_ctx_set_comm_rehearsal), the GPU to "
+                    "itself: value x G estimates an N = G node (exchanges free); its proofs are not valid")
+    a = ap.parse_args()
+    os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    spx = bench.load_product()
+    G, B, P = a.G, a.inflight, a.proofs
+    world = G
+    if a.solo:
+        G = 1  # one rank object, acting as rank 0 of `world`
+    groups = [spx.CommGroup(G) for _ in range(B)]
+    ctxs = [[spx.Context(0) for _ in range(B)] for _ in range(G)]
+    for r in range(G):
+        for k in range(B):
+            if a.solo:
+                ctxs[r][k].set_comm_rehearsal(0, world)
+            elif G > 1:
+                ctxs[r][k].set_comm_group(groups[k], r)
+    n = 1 << a.log_n
+    syn, mats, zs, nnz = bench.synth_instance(spx, 3, a.log_n, a.log_v, 0x5EED0000 + a.log_n, P, 0xB0B0)
+    pp = spx.MLProofForR1CS.setup(ctxs[0][0], a.log_n, 0xC0FFEE)
+    pks = [None] * G
+
+    def build(r):
+        pks[r] = spx.IndexPK(ctxs[r][0], bench.index_from_c(spx, ctxs[r][0], mats), a.log_n)
+
+    ths = [threading.Thread(target=build, args=(r,)) for r in range(G)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    wits = [spx.Witness(ctxs[0][0], z[: 32 << a.log_v], z[32 << a.log_v :]) for z in zs]
+    del zs
+
+    def run(steps):
+        out = [None] * G
+        errs = []
+
+        def rank(r):
+            try:
+                out[r] = spx.MLArgumentForR1CS.prove_many(ctxs[r], pks[r], wits * steps, pp, cached=a.cached)
+            except Exception as e:
+                errs.append(repr(e))
+
+        t = [threading.Thread(target=rank, args=(r,)) for r in range(G)]
+        t0 = time.perf_counter()
+        [x.start() for x in t]
+        [x.join() for x in t]
+        el = time.perf_counter() - t0
+        assert not errs, errs
+        assert all(o == out[0] for o in out), "ranks disagree"
+        return out[0], el
+
+    if a.warmup:
+        run(a.warmup)
+    proofs, el = run(a.steps)
+    print(json.dumps({"G": world, "solo_rank0": a.solo, "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
+                      "value": round(a.steps * P * n / el, 1), "ms_per_proof": round(el / (a.steps * P) * 1e3, 3),
+                      # strong scaling: every rank works on every proof, so the node finishes the batch when
+                      # rank 0 does (ranks are symmetric; exchanges taken as free)
+                      "node_estimate": round(a.steps * P * n / el, 1) if a.solo else None,
+                      "distinct": len(set(proofs)),
+                      "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -44,6 +44,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # instruction issues over 2 cycles on a SIMD-32; = the 157.3 TFLOPS FP32 vector spec / 2 per FMA)
 VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 2.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_kernels.json")
+# the same passes over the C2 workload (2^18, commitment stubbed): its launches' own counters
+PMC_FILE_C2 = os.path.join(ROOT, "profiles", "pmc_kernels_c2.json")
 ISSUE_FILE = os.path.join(ROOT, "profiles", "r02_ubench_issue.txt")
 MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
@@ -57,10 +59,12 @@ HBM_KERNELS = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expa
 KIND_NAMES = {0: "uniform-3n", 1: "ref-shaped", 3: "circuit-3n"}
 
 
-def pmc_kernel(kname):
+def pmc_kernel(kname, path=PMC_FILE):
     """per-launch counters of `kname` from the committed rocprofv3 PMC passes (tools/pmc_summary.py)"""
+    if not path:
+        return None
     try:
-        d = json.load(open(PMC_FILE))
+        d = json.load(open(path))
     except (OSError, ValueError):
         return None
     sym = KSYM.get(kname)
@@ -316,10 +320,11 @@ def madd_register_resident():
     return None
 
 
-def roofline_hbm(stats):
+def roofline_hbm(stats, pmc_path=PMC_FILE):
     """dominant HBM-streaming kernel (largest device time per proof among the sumcheck / SpMV / eq / fold
     kernels), priced on its largest launches (round 1: the tables stream from HBM; later rounds shrink
-    into the caches and are launch-latency bound)"""
+    into the caches and are launch-latency bound). `traffic` comes from the PMC passes over the SAME
+    workload (pmc_path), or is null when there is none."""
     cands = [k for k in HBM_KERNELS if k in stats]
     if not cands:
         return None
@@ -329,7 +334,7 @@ def roofline_hbm(stats):
     avg_s = big["ms"] / big["launches"] / 1e3
     per_launch = big["bytes"] / big["launches"]
     ach = per_launch / avg_s / 1e9
-    pm = pmc_kernel(dom) or {}
+    pm = pmc_kernel(dom, pmc_path) or {}
     return {"kernel": KSYM.get(dom, dom), "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pm.get("traffic_bytes_largest"),
             "bytes_per_launch": per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
@@ -363,6 +368,11 @@ def main():
                     help="N > 1 headline: 'proof' = every proof split over all ranks (strong, per-round exchange); "
                     "'batch' = every rank proves its own proofs (weak, no data-path exchange)")
     ap.add_argument("--no-other", action="store_true", help="N > 1: skip the other shard mode's measurement")
+    ap.add_argument("--groups", default="2",
+                    help="N >= 4: also measure proof groups of these sizes K (N / K groups of K ranks, every proof sharded "
+                    "over its group's K GPUs); '' to skip")
+    ap.add_argument("--rehearse", default="2,4,8",
+                    help="N = 1: world sizes G for the one-rank rehearsal of a G-GPU proof-sharded node ('' to skip)")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
                     help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (needs --inflight 1)")
     ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts)")
@@ -523,13 +533,60 @@ def main():
             p4, el1 = timed(single_fn(octxs[0], opk))
             assert p4 == ref[0], "proof-sharded single proof differs"
         other = [el, el1]
+    # ---- N >= 4: proof groups (every proof sharded over K ranks, N / K groups side by side)
+    grouped = {}
+    if world >= 4 and not args.no_other and args.groups and not stub:
+        for K in [int(x) for x in args.groups.split(",") if x.strip()]:
+            if K < 2 or K >= world or world % K:
+                continue
+            gname = [spx.shm_name() if rank == 0 else None]
+            dist.broadcast_object_list(gname, src=0)
+            gctxs = [spx.Context(device) for _ in range(B)]
+            for j, c in enumerate(gctxs):
+                c.set_comm_shm("%s_g%d_%d" % (gname[0], rank // K, j), rank % K, K)
+            gpk = spx.IndexPK(gctxs[0], index_from_c(spx, gctxs[0], mats), log_n)
+            batch_fn(gctxs, gpk, 1)()
+            pg, elg = timed(batch_fn(gctxs, gpk, args.steps))
+            check_batch(pg, ref)
+            grouped[K] = elg
+            del gctxs, gpk
+
+    # ---- N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank (rank 0 of G) of every
+    # proof, with no peers: every exchange returns its own contribution (spx_ctx_set_comm_rehearsal), so
+    # the rank does a real rank's device and host work for its 1/G of the buckets, blocks and hashing.
+    # Every rank of the node does the same on its own GPU, so the node's rate is this rank's proof rate
+    # (exchange latency taken as free; the proofs of a rehearsal are not valid and are not checked).
+    rehearsal = None
+    if world == 1 and args.rehearse and not stub:
+        rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free); "
+                     "node value = the rank's proof rate x n", "proofs_in_flight": B, "values": {}, "msm_reruns": {}}
+        for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
+            rc = [spx.Context(device) for _ in range(B)]
+            for c in rc:
+                c.set_comm_rehearsal(0, G)
+            rk = spx.IndexPK(rc[0], index_from_c(spx, rc[0], mats), log_n)
+            wl = [wits[i % W] for i in range(P)]
+            spx.MLArgumentForR1CS.prove_many(rc, rk, wl, pp, mode=args.mode, seed=7)
+            t0 = time.perf_counter()
+            spx.MLArgumentForR1CS.prove_many(rc, rk, wl * args.steps, pp, mode=args.mode, seed=7)
+            el = time.perf_counter() - t0
+            rehearsal["values"][str(G)] = round(P * args.steps * n / el, 1)
+            rehearsal["msm_reruns"][str(G)] = sum(c.msm_reruns() for c in rc)
+            del rk, rc
 
     ms = elapsed / args.steps * 1e3  # per step (P proofs)
     ms_c = elapsed_cached / args.steps * 1e3 if elapsed_cached else 0.0
     ms_1 = elapsed_single / args.steps * 1e3
     ms_1c = elapsed_single_c / args.steps * 1e3 if elapsed_single_c else 0.0
     ms_o = ms_o1 = None
+    ms_g = {}
     if dist is not None:
+        import torch
+
+        for K in sorted(grouped):  # max over ranks, in the same order on every rank
+            tg = torch.tensor([grouped[K] / args.steps * 1e3], dtype=torch.float64)
+            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+            ms_g[K] = float(tg[0])
         import torch
 
         t = torch.tensor([ms, ms_c, ms_1, ms_1c, (other[0] / args.steps * 1e3) if other else 0.0,
@@ -548,14 +605,14 @@ def main():
     roof = None
     if alone:
         if stub:
-            roof = roofline_hbm(alone)
+            roof = roofline_hbm(alone, PMC_FILE_C2 if log_n == 18 else None)
         else:
             dom = "msm_acc_g2" if "msm_acc_g2" in alone else max(alone, key=lambda k: alone[k]["ms"])
             roof = roofline_valu(alone, dom)
             if dom in stats:  # the same kernel while 16 proofs share the GPU
                 d = stats[dom]
                 roof["avg_launch_us_shared"] = round(d["ms"] / d["launches"] * 1e3, 2)
-            hb = roofline_hbm(alone)
+            hb = roofline_hbm(alone, PMC_FILE if log_n == 20 else None)
             if hb:
                 roof["hbm_kernels"] = hb
             if world == 1:
@@ -634,6 +691,11 @@ def main():
     out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
                    "hashing_s_per_proof": round(hash_s, 4),
                    "hashing_cores_busy": round(jobs / (ms / 1e3) * hash_s, 2)}
+    for K, mg in ms_g.items():
+        out.setdefault("value_proof_groups", {})[str(K)] = {
+            "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),
+            "layout": "%d groups of %d ranks, every proof sharded over its group (%d proofs per group per step)" % (
+                world // K, K, P)}
     if ms_o is not None:
         if sharded_head:  # the other mode: every rank proves whole proofs
             out["value_batch_weak"] = round(P * world * n / (ms_o / 1e3), 1)
@@ -642,6 +704,9 @@ def main():
             out["value_proof_sharded"] = round(P * n / (ms_o / 1e3), 1)
             out["ms_per_step_proof_sharded"] = round(ms_o, 3)
             out["ms_per_proof_single_proof_sharded"] = round(ms_o1, 3) if ms_o1 else None
+    if rehearsal:
+        rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
+        out["proof_sharded_rehearsal"] = rehearsal
     if not stub and world == 1 and not args.no_c2:
         out["c2"] = c2_line(spx, L, args, B)
     print(json.dumps(out), flush=True)
@@ -691,7 +756,7 @@ def c2_line(spx, L, args, B):
         "ms_per_proof_single_cached_transcript": round(el1 * 1e3, 3),
         "value_index_cached_transcript": round(steps * P * n / elc, 1),
         "kernels_ms_per_proof": {k: round(v["ms"], 4) for k, v in stats.items()},
-        "roofline": roofline_hbm(stats),
+        "roofline": roofline_hbm(stats, PMC_FILE_C2),
     }
     if not args.no_cpu:
         res["cpu_baseline_all_cores"] = cpu_baseline(3, log_n, log_v, args.cpu_seconds, threads=host_cores(), stub=True,

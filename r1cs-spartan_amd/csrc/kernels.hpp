@@ -132,6 +132,11 @@ void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr
 void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
                       Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s);
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
+// the last levels of an opening in one launch: how many of the `remaining` levels starting at a level
+// of `half` pairs it takes (0: none), and the launch (points[j] folds level j; q receives the levels'
+// quotients contiguously; `last` the final value)
+int open_tail_levels(uint64_t half, int remaining);
+void launch_open_tail(const Fr* rin, Fr* q, uint64_t half, int nlev, const Fr* points, Fr* last, hipStream_t s);
 
 // ---- msm.hip
 // One MSM inside a batch. Bases are the PRECOMPUTED window copies of a base set:

@@ -13,6 +13,7 @@
 // straight into the host's pinned memory.
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <stdexcept>
 
 namespace spx {
@@ -69,36 +70,82 @@ __global__ __launch_bounds__(kThreads) void k_reduce_partials(const Fr* __restri
     block_reduce_store<K>(acc, out);
 }
 
-// Last-block reduction (one launch per sumcheck round instead of two): every block stores its K
-// partials, then takes a ticket; the block drawing the last ticket sums all partials in block order
-// (field addition is exact: the same element as k_reduce_partials) into `out` (may be host-mapped
-// pinned memory, read by the host after the stream sync) and resets the ticket for the next launch.
+// Last-block reduction (one launch per sumcheck round instead of two). The per-XCD L2s are not
+// coherent, and a __threadfence() per block (an L2 write-back + L1 invalidate, several us each) cost
+// more than the launch it saves; so the hand-off follows the guide's write-through form
+// (cdna_hip_programming.md §6 G16): each block's thread 0 stores its K partials with agent-scope
+// (sc1, write-through) stores, drains them (s_waitcnt vmcnt(0)), then takes a ticket; the block that
+// draws the last ticket reads every partial with agent-scope (sc1) loads, sums them in block order
+// (field addition is exact: the same element as a separate reduction launch) into `out` (may be
+// host-mapped pinned memory, read after the stream sync) and resets the ticket.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+template <int K>
+DEV void block_reduce(Fr (&acc)[K]) {  // result valid in thread 0
+    __shared__ Fr lds[K][kThreads / 64];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Fr o = shfl_xor(acc[k], m);
+            fe_add(acc[k], acc[k], o);
+        }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[k][wid] = acc[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Fr s = lds[k][0];
+            for (int w = 1; w < (int)(blockDim.x / 64); ++w) fe_add(s, s, lds[k][w]);
+            acc[k] = s;
+        }
+    }
+    __syncthreads();  // lds may be reused by the caller's next reduction
+}
 template <int K>
 DEV void grid_reduce_last(Fr (&acc)[K], Fr* __restrict__ partial, uint32_t* __restrict__ ticket, Fr* __restrict__ out) {
-    block_reduce_store<K>(acc, partial + (size_t)blockIdx.x * K);
+    block_reduce<K>(acc);
     __shared__ bool last;
     if (threadIdx.x == 0) {
-        __threadfence();  // this block's partial is visible device-wide before its ticket
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        gu64* dst = (gu64*)(partial + (size_t)blockIdx.x * K);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                __hip_atomic_store(dst + 4 * k + w, (unsigned long long)acc[k].v[2 * w] | ((unsigned long long)acc[k].v[2 * w + 1] << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has left this CU before the ticket
+        last = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();  // acquire: every other block's partial
 #pragma unroll
     for (int k = 0; k < K; ++k) fe_zero(acc[k]);
     for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+        const gu64* src = (const gu64*)(partial + (size_t)b * K);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             Fr v;
-            const Fr* src = partial + (size_t)b * K + k;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v.v[i] = __builtin_nontemporal_load(&src->v[i]);
+            for (int w = 0; w < 4; ++w) {
+                const unsigned long long x = __hip_atomic_load(src + 4 * k + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v.v[2 * w] = (uint32_t)x;
+                v.v[2 * w + 1] = (uint32_t)(x >> 32);
+            }
             fe_add(acc[k], acc[k], v);
         }
     }
-    __syncthreads();  // the shared scratch of the first block_reduce_store is free again
-    block_reduce_store<K>(acc, out);
-    if (threadIdx.x == 0) *ticket = 0u;
+    block_reduce<K>(acc);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) st_fr(out + k, acc[k]);
+        *ticket = 0u;
+    }
 }
 
 // ------------------------------------------------------------------ conversions
@@ -378,6 +425,41 @@ __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ 
     }
 }
 
+// The last levels of an opening in ONE launch (one block, the table in LDS): level j folds
+// half = h0 >> j pairs, q_j = the level's quotients (q + qoff_j, contiguous), r' as k_open_level.
+// The final one-entry table goes to `last`. (Launched per level these small folds were latency: one
+// launch gap each.)
+static constexpr int kTailMax = 512;  // largest first half of the tail (LDS: 2 x 512 Fr)
+struct TailPoints {
+    Fr p[kTailMax <= 512 ? 10 : 20];
+};
+__global__ __launch_bounds__(kTailMax) void k_open_tail(const Fr* __restrict__ rin, Fr* __restrict__ q, uint32_t h0,
+                                                        int nlev, TailPoints pts, Fr* __restrict__ last) {
+    __shared__ Fr buf[2 * kTailMax];
+    for (uint32_t b = threadIdx.x; b < 2 * h0; b += blockDim.x) buf[b] = ld_fr(rin + b);
+    __syncthreads();
+    uint32_t half = h0;
+    Fr* qj = q;
+    for (int j = 0; j < nlev; ++j) {
+        Fr t;
+        const uint32_t b = threadIdx.x;
+        if (b < half) {
+            const Fr a0 = buf[2 * b], a1 = buf[2 * b + 1];
+            Fr d;
+            fe_sub(d, a1, a0);
+            if (q) st_fr(qj + b, d);
+            fe_mul(t, d, pts.p[j]);
+            fe_add(t, a0, t);
+        }
+        __syncthreads();
+        if (b < half) buf[b] = t;
+        __syncthreads();
+        qj += half;
+        half >>= 1;
+    }
+    if (threadIdx.x == 0) st_fr(last, buf[0]);
+}
+
 // ------------------------------------------------------------------ launchers
 static inline int grid_for(uint64_t n, int cap = 2048) {
     uint64_t g = (n + kThreads - 1) / kThreads;
@@ -457,6 +539,22 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
         hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
                            ticket, result3);
     kp_end(32.0 * (double)half * (fold ? 12.0 : 4.0), s);
+}
+
+int open_tail_levels(uint64_t half, int remaining) {
+    if (half > (uint64_t)kTailMax || remaining < 2) return 0;
+    int k = 0;
+    while ((half >> k) >= 1 && k < remaining) ++k;
+    return std::min(k, (int)(sizeof(TailPoints) / sizeof(Fr)));
+}
+void launch_open_tail(const Fr* rin, Fr* q, uint64_t half, int nlev, const Fr* points, Fr* last, hipStream_t s) {
+    TailPoints tp{};
+    if (nlev < 1 || nlev > (int)(sizeof(TailPoints) / sizeof(Fr)) || half > (uint64_t)kTailMax || (half >> (nlev - 1)) < 1)
+        throw std::invalid_argument("launch_open_tail: bad level range");
+    for (int j = 0; j < nlev; ++j) tp.p[j] = points[j];
+    kp_begin(KP_OPEN, s);
+    hipLaunchKernelGGL(k_open_tail, dim3(1), dim3(kTailMax), 0, s, rin, q, (uint32_t)half, nlev, tp, last);
+    kp_end(32.0 * 4.0 * (double)half, s);  // read 2, write q and r' per pair, over the levels: <= 4 x half
 }
 
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s) {

@@ -69,7 +69,7 @@ template <bool COMPACT>
 __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
                                                      int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t cap,
-                                                     uint32_t* __restrict__ st) {
+                                                     uint32_t* __restrict__ st, uint32_t* __restrict__ hist) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = g < total;
     if (!COMPACT && !live) return;
@@ -93,6 +93,7 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
             const uint64_t o = I.ref_off + (uint64_t)w * I.size + j;
             keys[o] = key == ~0u ? nb : key;
             vals[o] = digit_ref(I, w, j, d);
+            if (hist && key != ~0u) atomicAdd(&hist[key], 1u);
         }
     } else {
         uint32_t cnt = 0;
@@ -121,14 +122,13 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                 if (pos < cap) {
                     keys[pos] = key;
                     vals[pos] = digit_ref(I, w, j, dg);
+                    if (hist) atomicAdd(&hist[key], 1u);
                 }
                 ++pos;
             }
         }
-        if (threadIdx.x == 0) {
-            __threadfence();
+        if (threadIdx.x == 0)  // (its cursor add has returned: every block's slots are taken when the last ticket is)
             last = atomicAdd(&st[2], 1u) == gridDim.x - 1;
-        }
         __syncthreads();
         if (last) {  // every block has taken its slots: fill the rest
             const uint32_t used = min(atomicAdd(&st[1], 0u), cap);
@@ -154,41 +154,50 @@ __global__ __launch_bounds__(kLight) void k_bucket_bounds(const uint32_t* __rest
     offs[b] = (uint32_t)lo;
 }
 
-// One block: v[b] = f(b) for b < nb, v[nb] = 0; vals = v (optional), offs = exclusive prefix sums.
-// MODE 0 (partials of the affine level): f(b) = the seg-length thread ranges bucket b's references
-// [off[b], off[b + 1]) meet; MODE 1 (XYZZ level): f(b) = ceil(cnt[b] / seg).
-static constexpr int kScanThreads = 1024;
-template <int MODE>
-__global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restrict__ in, uint32_t nb, uint32_t seg,
-                                                        uint32_t* __restrict__ vals, uint32_t* __restrict__ offs) {
-    auto f = [&](uint32_t b) -> uint32_t {
+// Counting sort's scatter: bucket b's references go to [offs[b], offs[b] + cnt[b]) in any order (group
+// addition is exact and commutative), each slot taken by decrementing the bucket's count.
+__global__ __launch_bounds__(kLight) void k_bucket_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                           uint64_t n, uint32_t nb, const uint32_t* __restrict__ offs,
+                                                           uint32_t* __restrict__ cnt, uint32_t* __restrict__ refs) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = keys[i];
+    if (k >= nb) return;
+    refs[offs[k] + atomicSub(&cnt[k], 1u) - 1u] = vals[i];
+}
+
+// Exclusive offsets of a per-bucket count derived from the previous offsets (device-wide hipCUB
+// scan over a transform iterator: no count array, no extra launch). Counts are off[b + 1] - off[b].
+struct PartialsOp {  // the seg-length thread ranges bucket b's references [off[b], off[b + 1]) meet
+    const uint32_t* off;
+    uint32_t nb, seg;
+    __host__ __device__ uint32_t operator()(uint32_t b) const {
         if (b >= nb) return 0u;
-        if (MODE == 0) {
-            const uint32_t o = in[b], c = in[b + 1] - o;
-            return c ? (o + c - 1) / seg - o / seg + 1 : 0u;
-        }
-        return (in[b] + seg - 1) / seg;
-    };
-    const uint32_t per = (nb + 1 + kScanThreads - 1) / kScanThreads;
-    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb + 1);
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += f(b);
-    using Scan = hipcub::BlockScan<uint32_t, kScanThreads>;
-    __shared__ typename Scan::TempStorage tmp;
-    uint32_t pre;
-    Scan(tmp).ExclusiveSum(sum, pre);
-    for (uint32_t b = b0; b < b1; ++b) {
-        const uint32_t v = f(b);
-        if (vals) vals[b] = v;
-        offs[b] = pre;
-        pre += v;
+        const uint32_t o = off[b], c = off[b + 1] - o;
+        return c ? (o + c - 1) / seg - o / seg + 1 : 0u;
     }
+};
+struct SegsOp {  // segments of `seg` partials for bucket b's partials [off[b], off[b + 1])
+    const uint32_t* off;
+    uint32_t nb, seg;
+    __host__ __device__ uint32_t operator()(uint32_t b) const {
+        return b < nb ? (off[b + 1] - off[b] + seg - 1) / seg : 0u;
+    }
+};
+template <class Op>
+static void scan_op(MsmWorkspace* ws, const Op& op, uint32_t nb, uint32_t* out, hipStream_t s) {
+    hipcub::CountingInputIterator<uint32_t> cit(0u);
+    hipcub::TransformInputIterator<uint32_t, Op, hipcub::CountingInputIterator<uint32_t>> it(cit, op);
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, it, out, (int)nb + 1, s));
+    void* t = ws->cub.ensure(tb);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, it, out, (int)nb + 1, s));
 }
-void launch_scan_partials(const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np, uint32_t* np_off, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan1<0>, dim3(1), dim3(kScanThreads), 0, s, offs, nb, seg, np, np_off);
+void scan_partials(MsmWorkspace* ws, const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np_off, hipStream_t s) {
+    scan_op(ws, PartialsOp{offs, nb, seg}, nb, np_off, s);
 }
-void launch_scan_segs(const uint32_t* cnt, uint32_t nb, uint32_t seg, uint32_t* segcnt, uint32_t* seg_off, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan1<1>, dim3(1), dim3(kScanThreads), 0, s, cnt, nb, seg, segcnt, seg_off);
+void scan_segs(MsmWorkspace* ws, const uint32_t* off, uint32_t nb, uint32_t seg, uint32_t* seg_off, hipStream_t s) {
+    scan_op(ws, SegsOp{off, nb, seg}, nb, seg_off, s);
 }
 
 uint32_t seg1_len(bool g2) {
@@ -362,21 +371,41 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * std::max<uint64_t>(n, 1));
     uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
     const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
+    // SPX_MSM_SORT=count: counting sort (histogram atomics in the keys pass, scan, scatter), no
+    // decoupled look-back; default: hipCUB's radix sort (onesweep)
+    static const bool count_sort = [] {
+        const char* e = getenv("SPX_MSM_SORT");
+        return e && std::string(e) == "count";
+    }();
+    uint32_t* hist = nullptr;
+    if (count_sort) {
+        hist = (uint32_t*)ws->hist.ensure(4 * (nb + 1));
+        HIPCHK(hipMemsetAsync(hist, 0, 4 * (nb + 1), s));
+    }
     kp_begin(KP_SORT, s);
     if (p.compact)
         hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, (uint32_t)n, st);
+                           scalars, ka, va, (uint32_t)n, st, hist);
     else
         hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, 0u, st);
-    hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
-    void* t = ws->cub.ensure(tb);
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
-    o.refs = dv.Current();
-    hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, dk.Current(), n, nb,
-                       o.offs);
+                           scalars, ka, va, 0u, st, hist);
+    if (count_sort) {
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hist, o.offs, (int)nb + 1, s));
+        void* t = ws->cub.ensure(tb);
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, hist, o.offs, (int)nb + 1, s));
+        hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, ka, va, n, nb,
+                           o.offs, hist, o.refs);
+    } else {
+        hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
+        void* t = ws->cub.ensure(tb);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
+        o.refs = dv.Current();
+        hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, dk.Current(), n, nb,
+                           o.offs);
+    }
     kp_end(32.0 * p.tot_sc + 4.0 * 8 * n, s);
     return o;
 }

@@ -113,7 +113,7 @@ struct PinArena {
 };
 
 struct MsmWorkspace {
-    DBuf tables, offs, refs, segcnt, spare, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a;
+    DBuf tables, offs, refs, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a, hist;
     // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
     // rank's buckets (e.g. many equal values) stops overflowing after its first batch
     double cap_scale = 1.0;
@@ -152,10 +152,10 @@ struct MsmSorted {
     uint32_t *offs, *refs;
 };
 MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* status_words, hipStream_t s);
-// partials of the load-balanced affine level per bucket (the seg-length thread ranges its references
-// meet) and their exclusive offsets, in one launch
-void launch_scan_partials(const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np, uint32_t* np_off, hipStream_t s);
-// next XYZZ level: segments of `seg` partials per bucket and their exclusive offsets, in one launch
-void launch_scan_segs(const uint32_t* cnt, uint32_t nb, uint32_t seg, uint32_t* segcnt, uint32_t* seg_off, hipStream_t s);
+// exclusive offsets of the load-balanced affine level's partials per bucket (the seg-length thread
+// ranges a bucket's references [offs[b], offs[b + 1]) meet); np_off[nb] = all partials
+void scan_partials(MsmWorkspace* ws, const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np_off, hipStream_t s);
+// exclusive offsets of the next XYZZ level: segments of `seg` partials per bucket
+void scan_segs(MsmWorkspace* ws, const uint32_t* off, uint32_t nb, uint32_t seg, uint32_t* seg_off, hipStream_t s);
 
 }  // namespace spx

@@ -337,7 +337,6 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
 template <class F>
 __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uint32_t* __restrict__ segoff, uint32_t nb,
                                                                        const uint32_t* __restrict__ off,
-                                                                       const uint32_t* __restrict__ cnt,
                                                                        const Xyzz<F>* __restrict__ in,
                                                                        Xyzz<F>* __restrict__ out) {
     using A = Acc<F>;
@@ -347,7 +346,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_xyzz(const uin
     const uint32_t b = find_bucket(segoff, nb, s);
     const uint32_t k = s - segoff[b];
     const uint32_t start = off[b] + k * kSeg;
-    const uint32_t end = min(start + kSeg, off[b] + cnt[b]);
+    const uint32_t end = min(start + kSeg, off[b + 1]);  // bucket b's partials: [off[b], off[b + 1])
     X29<T> acc;
     A::ld(acc, in + start);
     for (uint32_t e = start + 1; e < end; ++e) {
@@ -379,7 +378,7 @@ DEV uint32_t tree_chunk_log(uint32_t lb) { return lb - 1 < kTreeChunkLog ? lb - 
 template <class F>
 __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     const MsmInst* __restrict__ insts, const uint64_t* __restrict__ wp, int ninst, const uint32_t* __restrict__ node_off,
-    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, const Xyzz<F>* __restrict__ P,
+    const uint32_t* __restrict__ off, const Xyzz<F>* __restrict__ P,
     Xyzz<F>* __restrict__ Fo, Xyzz<F>* __restrict__ So, Xyzz<F>* __restrict__ Do) {
     using A = Acc<F>;
     const uint64_t t = tree_elem<F>();
@@ -397,7 +396,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
     x29_set_inf(run);
     const int m = 1 << lgm;
     int j = m - 1;
-    uint32_t u = 0, nu = cnt[b0 + j];  // partials of bucket j added so far / to add
+    uint32_t u = 0, nu = off[b0 + j + 1] - off[b0 + j];  // partials of bucket j added so far / to add
 #pragma unroll 1
     for (;;) {
         const bool bucket_step = u < nu;
@@ -411,7 +410,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
             if (j == 0) break;
             --j;
             u = 0;
-            nu = cnt[b0 + j];
+            nu = off[b0 + j + 1] - off[b0 + j];
             continue;
         } else {
             A::ld(a, Fo + o);
@@ -425,7 +424,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_chunk(
             if (j == 0) break;
             --j;
             u = 0;
-            nu = cnt[b0 + j];
+            nu = off[b0 + j + 1] - off[b0 + j];
         }
     }
     A::st(So + o, run);
@@ -588,11 +587,9 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
-    uint32_t* cur_cnt = (uint32_t*)ws->segcnt.ensure(4 * (nb + 1));
-    uint32_t* spare_cnt = (uint32_t*)ws->spare.ensure(4 * (nb + 1));
     uint32_t* cur_off = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
     uint32_t* nxt_off = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
-    launch_scan_partials(so.offs, nb, kSeg1, cur_cnt, cur_off, s);
+    scan_partials(ws, so.offs, nb, kSeg1, cur_off, s);
     const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, cur_off, so.refs, pts, PA,
@@ -609,15 +606,13 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     const double mu = pl.mu_max;
     uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1;  // partials per bucket
     while (m > 1) {
-        launch_scan_segs(cur_cnt, nb, kSeg, spare_cnt, nxt_off, s);
+        scan_segs(ws, cur_off, nb, kSeg, nxt_off, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
-        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur_cnt,
-                           cur, nxt);
+        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur, nxt);
         kp_end((double)(cur_max_segs + nsegs) * psz, s, (double)cur_max_segs);
         std::swap(cur, nxt);
         std::swap(cur_off, nxt_off);
-        std::swap(cur_cnt, spare_cnt);
         cur_max_segs = nsegs;
         m = (m + kSeg - 1) / kSeg;
     }
@@ -632,7 +627,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     {
         uint64_t work = pl.wp[nact];
         hipLaunchKernelGGL(k_tree_chunk<F>, dim3(tree_blocks<F>(work)), dim3(kHeavy), 0, s, pl.d_insts, pl.d_wp, nact,
-                           pl.d_noff, cur_cnt, cur_off, cur, A3[0], A3[1], A3[2]);
+                           pl.d_noff, cur_off, cur, A3[0], A3[1], A3[2]);
     }
     for (int lv = 1; lv < pl.top_from; ++lv) {
         uint64_t work = 3 * pl.wp[(size_t)lv * (nact + 1) + nact];

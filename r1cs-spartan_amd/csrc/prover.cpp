@@ -775,11 +775,21 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
     std::vector<MsmInst> insts(L - first);
     const Fr* rin = z;
     uint64_t qoff = 0;
+    int tail_from = L;  // levels >= tail_from fold in one launch (open_tail_levels)
     for (int i = 0; i < L; ++i) {
         const uint64_t half = n >> (i + 1);
-        Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, q + qoff, dev_fr(point[i]), half, C.stream);
-        rin = rout;
+        if (i >= first && i < tail_from && open_tail_levels(half, L - i) == L - i) {
+            std::vector<Fr> pts(L - i);
+            for (int j = i; j < L; ++j) pts[j - i] = dev_fr(point[j]);
+            Fr* last = bufs[i & 1];
+            launch_open_tail(rin, q + qoff, half, L - i, pts.data(), last, C.stream);
+            tail_from = i;
+            rin = last;
+        } else if (i < tail_from) {
+            Fr* rout = bufs[i & 1];
+            launch_open_level(rin, rout, q + qoff, dev_fr(point[i]), half, C.stream);
+            rin = rout;
+        }
         if (i < first) continue;  // fold only; the level's proof is proof0 (its quotient is overwritten next)
         MsmInst& I = insts[i - first];
         I.pts_off = P.g2_off[i];
@@ -828,7 +838,15 @@ static OpenOut open_stub(Ctx& C, const Fr* z_local, int L, const std::vector<HFr
     const Fr* rin = z_local;
     for (int i = 0; i < nloc; ++i) {
         Fr* rout = bufs[i & 1];
-        launch_open_level(rin, rout, nullptr, dev_fr(point[i]), nl >> (i + 1), C.stream);
+        const uint64_t half = nl >> (i + 1);
+        if (open_tail_levels(half, nloc - i) == nloc - i) {  // the remaining levels in one launch
+            std::vector<Fr> pts(nloc - i);
+            for (int j = i; j < nloc; ++j) pts[j - i] = dev_fr(point[j]);
+            launch_open_tail(rin, nullptr, half, nloc - i, pts.data(), rout, C.stream);
+            rin = rout;
+            break;
+        }
+        launch_open_level(rin, rout, nullptr, dev_fr(point[i]), half, C.stream);
         rin = rout;
     }
     SPX_HIP(hipMemcpyAsync(h + 32 * L, rin, 32, hipMemcpyDeviceToHost, C.stream));

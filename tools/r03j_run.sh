@@ -3,7 +3,7 @@ set -eo pipefail
 export TMPDIR=/tmp
 cd /tmp
 R=$GRAFT_REPO_ROOT
-for G in 1 8; do
+for G in ${TRACE_GS:-1 8}; do
   timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/sj_$G -o run --output-format csv -- \
      python3 $R/tools/vrank_bench.py --G $G --inflight 16 --cached --solo --proofs 64 --warmup 1 >> $R/gpurun_out/r03j_solo.jsonl 2>> $R/gpurun_out/r03j_solo.err
   f=$(find /tmp/sj_$G -name "*kernel_trace.csv" | head -1)

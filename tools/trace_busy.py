@@ -47,6 +47,18 @@ for s, e, name, grid, wg in ev:
     fam[short][1] += min(waves, 1024) * d
     fam[short][2] += 1
 print("span %.1f ms, >=1 kernel running %.1f%%, kernels %d" % (span / 1e6, 100 * busy / span, len(ev)))
+# concurrency: time-weighted number of kernels running at once (hardware queues bound it)
+pts = sorted([(s, 1) for s, e, *_ in ev] + [(e, -1) for s, e, *_ in ev])
+hist = defaultdict(float)
+cur, last = 0, pts[0][0] if pts else 0
+for t, d in pts:
+    hist[cur] += t - last
+    cur += d
+    last = t
+tot_t = sum(hist.values()) or 1.0
+avg = sum(k * v for k, v in hist.items()) / tot_t
+print("concurrent kernels: time-weighted mean %.2f; share of time with >= k running: %s" % (
+    avg, " ".join("%d:%.0f%%" % (k, 100 * sum(v for c, v in hist.items() if c >= k) / tot_t) for k in (1, 2, 4, 8, 12, 16, 24, 32))))
 tot_occ = sum(v[1] for v in fam.values())
 print("SIMD-occupancy estimate (sum min(waves,1024) x duration / 1024 x span): %.1f%%" % (100 * tot_occ / (1024 * span)))
 for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])[: int(os.environ.get("TRACE_TOP", "20"))]:

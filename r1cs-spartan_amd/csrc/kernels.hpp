@@ -124,18 +124,24 @@ void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* 
 void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
                      Fr* scratch_hi, hipStream_t s);
 int sc_grid(uint64_t half);
-// One launch per round: fold with the previous challenge r (by value; unused in round 1), evaluate the
-// round polynomial at 0, 1, 2, and reduce over the blocks into result3 (3 Fr; device or host-mapped
-// pinned memory). partial: sc_grid(half) x 3 Fr of scratch; ticket: a device counter that is 0 (left 0).
+// A round: fold with the previous challenge r (by value; unused in round 1), evaluate the round
+// polynomial at 0, 1, 2 (at 1 only if need1: otherwise result3[1] = 0 and the caller derives it from
+// the previous claim), and reduce over the blocks into result3 (3 Fr; device or host-mapped pinned
+// memory) - in the last block for small grids, by a second one-block launch otherwise.
+// partial: sc_grid(half) x 3 Fr of scratch; ticket: a device counter that is 0 (left 0).
 void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
-                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s);
+                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s);
 void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
-                      Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s);
+                      Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s);
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
 // the last levels of an opening in one launch: how many of the `remaining` levels starting at a level
 // of `half` pairs it takes (0: none), and the launch (points[j] folds level j; q receives the levels'
 // quotients contiguously; `last` the final value)
 int open_tail_levels(uint64_t half, int remaining);
+// nf (2 or 3) consecutive levels in one launch: nout = the last level's table size; level j's
+// quotients go to q + qoffs[j] (~0: not written), points[j] folds level j
+void launch_open_fold(const Fr* rin, Fr* rout, Fr* q, int nf, const Fr* points, const uint64_t* qoffs, uint64_t nout,
+                      hipStream_t s);
 void launch_open_tail(const Fr* rin, Fr* q, uint64_t half, int nlev, const Fr* points, Fr* last, hipStream_t s);
 
 // ---- msm.hip

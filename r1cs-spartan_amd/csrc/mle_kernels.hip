@@ -294,11 +294,12 @@ __global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ l
 // FOLD == true  (round >= 2): X'[2b+u] = in[4b+2u] + r*(in[4b+2u+1] - in[4b+2u]) stored to out,
 //                             e = Ein[2b] + Ein[2b+1] stored to Eout[b]
 // partial[blk] = (G(0), G(1), G(2)) with G(t) = sum_b (A_t B_t - C_t) e,  X_2 = 2 X_1 - X_0.
-template <bool FOLD>
+// need1 == 0: G(1) is left 0 (the host derives it from the previous round's claim: P(0) + P(1) = claim).
+template <bool FOLD, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
                                                         Fr* __restrict__ Eout, const Fr r, uint64_t half,
                                                         Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
-                                                        Fr* __restrict__ result3) {
+                                                        Fr* __restrict__ result3, int need1) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -337,10 +338,12 @@ __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out,
         fe_mul(t, t, e);
         fe_add(g[0], g[0], t);
         // t = 1
-        fe_mul(t, x1[0], x1[1]);
-        fe_sub(t, t, x1[2]);
-        fe_mul(t, t, e);
-        fe_add(g[1], g[1], t);
+        if (need1) {
+            fe_mul(t, x1[0], x1[1]);
+            fe_sub(t, t, x1[2]);
+            fe_mul(t, t, e);
+            fe_add(g[1], g[1], t);
+        }
         // t = 2
         Fr y[3];
 #pragma unroll
@@ -353,16 +356,20 @@ __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out,
         fe_mul(t, t, e);
         fe_add(g[2], g[2], t);
     }
-    grid_reduce_last<3>(g, partial, ticket, result3);
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
 }
 
 // ------------------------------------------------------------------ sumcheck #2 round
-// tables M (= sum_m r_m M(r_x, .)) and Z; partial = (P(0), P(1), P(2)), P(t) = sum_b M_t Z_t.
-template <bool FOLD>
+// tables M (= sum_m r_m M(r_x, .)) and Z; partial = (P(0), P(1), P(2)), P(t) = sum_b M_t Z_t
+// (need1 == 0: P(1) left 0, derived on the host).
+template <bool FOLD, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
                                                         Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
                                                         uint64_t half, Fr* __restrict__ partial,
-                                                        uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+                                                        uint32_t* __restrict__ ticket, Fr* __restrict__ result3, int need1) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -397,8 +404,10 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
         Fr t, u, v;
         fe_mul(t, m0, z0);
         fe_add(g[0], g[0], t);
-        fe_mul(t, m1, z1);
-        fe_add(g[1], g[1], t);
+        if (need1) {
+            fe_mul(t, m1, z1);
+            fe_add(g[1], g[1], t);
+        }
         fe_add(u, m1, m1);
         fe_sub(u, u, m0);
         fe_add(v, z1, z1);
@@ -406,7 +415,10 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
         fe_mul(t, u, v);
         fe_add(g[2], g[2], t);
     }
-    grid_reduce_last<3>(g, partial, ticket, result3);
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
 }
 
 // ------------------------------------------------------------------ mKZG open level (open.rs:42-45)
@@ -422,6 +434,38 @@ __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ 
         fe_mul(t, d, p);
         fe_add(t, a0, t);
         st_fr(rout + b, t);
+    }
+}
+
+// NF consecutive levels of an opening in one launch: thread b takes the 2^NF entries
+// rin[2^NF b ..] and runs the NF folds in registers, writing level j's 2^(NF-1-j) quotients to
+// q_j = q + qoff[j] (j's quotients of this thread are contiguous; qoff[j] = ~0: not written) and the
+// last level's value to rout[b]. The intermediate tables never go to HBM (open.rs:42-45 per level).
+template <int NF>
+struct FoldArgs {
+    Fr p[NF];
+    uint64_t qoff[NF];
+};
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold(const Fr* __restrict__ rin, Fr* __restrict__ rout, Fr* __restrict__ q,
+                                                        FoldArgs<NF> a, uint64_t nout) {
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nout; b += (uint64_t)gridDim.x * blockDim.x) {
+        Fr v[1 << NF];
+#pragma unroll
+        for (int k = 0; k < (1 << NF); ++k) v[k] = ld_fr(rin + ((uint64_t)b << NF) + k);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const int m = 1 << (NF - 1 - j);  // this thread's pairs at level j
+#pragma unroll
+            for (int k = 0; k < m; ++k) {
+                Fr d, t;
+                fe_sub(d, v[2 * k + 1], v[2 * k]);
+                if (a.qoff[j] != ~0ull) st_fr(q + a.qoff[j] + (uint64_t)b * m + k, d);
+                fe_mul(t, d, a.p[j]);
+                fe_add(v[k], v[2 * k], t);
+            }
+        }
+        st_fr(rout + b, v[0]);
     }
 }
 
@@ -514,31 +558,53 @@ void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* 
 
 int sc_grid(uint64_t half) { return grid_for(half, 1024); }
 
+// Rounds whose grid has few blocks reduce in their last block (one launch); large grids keep a
+// separate one-block reduction launch, so the streaming kernel's own duration carries no serial tail.
+static constexpr int kFuseMaxBlocks = 64;
+template <bool FOLD>
+static void sc1_launch(int g, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r, uint64_t half,
+                       Fr* partial, uint32_t* ticket, Fr* result3, int need1, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc1_round<FOLD, true>), dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial,
+                           ticket, result3, need1);
+    else
+        hipLaunchKernelGGL((k_sc1_round<FOLD, false>), dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial,
+                           ticket, result3, need1);
+}
+template <bool FOLD>
+static void sc2_launch(int g, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half, Fr* partial,
+                       uint32_t* ticket, Fr* result3, int need1, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc2_round<FOLD, true>), dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
+                           ticket, result3, need1);
+    else
+        hipLaunchKernelGGL((k_sc2_round<FOLD, false>), dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half,
+                           partial, ticket, result3, need1);
+}
+
 void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
-                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
+                      uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC1, s);
     if (fold)
-        hipLaunchKernelGGL(k_sc1_round<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial, ticket,
-                           result3);
+        sc1_launch<true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     else
-        hipLaunchKernelGGL(k_sc1_round<false>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial, ticket,
-                           result3);
+        sc1_launch<false>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     // algorithmic bytes: fold reads 4 Fr x 3 tables + 2 E, writes 2 x 3 + 1 E; no fold reads 2 x 3 + 1
     kp_end(32.0 * (double)half * (fold ? (14.0 + 6.0 + (Eout ? 1.0 : 0.0)) : 7.0), s);
+    if (g > kFuseMaxBlocks) hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
 void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
-                      Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
+                      Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC2, s);
     if (fold)
-        hipLaunchKernelGGL(k_sc2_round<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
-                           ticket, result3);
+        sc2_launch<true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     else
-        hipLaunchKernelGGL(k_sc2_round<false>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
-                           ticket, result3);
+        sc2_launch<false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     kp_end(32.0 * (double)half * (fold ? 12.0 : 4.0), s);
+    if (g > kFuseMaxBlocks) hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
 }
 
 int open_tail_levels(uint64_t half, int remaining) {
@@ -555,6 +621,26 @@ void launch_open_tail(const Fr* rin, Fr* q, uint64_t half, int nlev, const Fr* p
     kp_begin(KP_OPEN, s);
     hipLaunchKernelGGL(k_open_tail, dim3(1), dim3(kTailMax), 0, s, rin, q, (uint32_t)half, nlev, tp, last);
     kp_end(32.0 * 4.0 * (double)half, s);  // read 2, write q and r' per pair, over the levels: <= 4 x half
+}
+
+void launch_open_fold(const Fr* rin, Fr* rout, Fr* q, int nf, const Fr* points, const uint64_t* qoffs, uint64_t nout,
+                      hipStream_t s) {
+    kp_begin(KP_OPEN, s);
+    const int g = grid_for(nout, 8192);
+    double qw = 0;
+    for (int j = 0; j < nf; ++j) qw += qoffs[j] != ~0ull ? (double)(nout << (nf - 1 - j)) : 0.0;
+    if (nf == 3) {
+        FoldArgs<3> a;
+        for (int j = 0; j < 3; ++j) a.p[j] = points[j], a.qoff[j] = qoffs[j];
+        hipLaunchKernelGGL(k_open_fold<3>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+    } else if (nf == 2) {
+        FoldArgs<2> a;
+        for (int j = 0; j < 2; ++j) a.p[j] = points[j], a.qoff[j] = qoffs[j];
+        hipLaunchKernelGGL(k_open_fold<2>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+    } else {
+        throw std::invalid_argument("launch_open_fold: 2 or 3 levels");
+    }
+    kp_end(32.0 * ((double)(nout << nf) + qw + (double)nout), s);  // read 2^nf per output, write quotients + 1
 }
 
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s) {

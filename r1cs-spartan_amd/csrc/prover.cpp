@@ -775,22 +775,42 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
     std::vector<MsmInst> insts(L - first);
     const Fr* rin = z;
     uint64_t qoff = 0;
-    int tail_from = L;  // levels >= tail_from fold in one launch (open_tail_levels)
-    for (int i = 0; i < L; ++i) {
+    // folds: groups of up to 3 levels per launch while the tables are large, then the last levels
+    // (<= 512 pairs) in one single-block launch; the fold-only level 0 (proof0 given) writes no quotient
+    std::vector<uint64_t> lvl_qoff(L, ~0ull);  // level i's quotients: q + lvl_qoff[i] (~0: not kept)
+    {
+        uint64_t o = 0;
+        for (int i = first; i < L; ++i) lvl_qoff[i] = o, o += n >> (i + 1);
+    }
+    int pp = 0;  // ping-pong: the next output buffer
+    for (int i = 0; i < L;) {
         const uint64_t half = n >> (i + 1);
-        if (i >= first && i < tail_from && open_tail_levels(half, L - i) == L - i) {
+        if (i >= first && open_tail_levels(half, L - i) == L - i) {
             std::vector<Fr> pts(L - i);
             for (int j = i; j < L; ++j) pts[j - i] = dev_fr(point[j]);
-            Fr* last = bufs[i & 1];
-            launch_open_tail(rin, q + qoff, half, L - i, pts.data(), last, C.stream);
-            tail_from = i;
+            Fr* last = bufs[pp];
+            launch_open_tail(rin, q + lvl_qoff[i], half, L - i, pts.data(), last, C.stream);
             rin = last;
-        } else if (i < tail_from) {
-            Fr* rout = bufs[i & 1];
-            launch_open_level(rin, rout, q + qoff, dev_fr(point[i]), half, C.stream);
-            rin = rout;
+            break;
         }
-        if (i < first) continue;  // fold only; the level's proof is proof0 (its quotient is overwritten next)
+        int nf = 1;  // levels in this launch: stop before the tail's start
+        while (nf < 3 && i + nf < L && open_tail_levels(n >> (i + nf + 1), L - i - nf) != L - i - nf) ++nf;
+        Fr* rout = bufs[pp];
+        pp ^= 1;
+        if (nf >= 2) {
+            Fr pts[3];
+            uint64_t qo[3];
+            for (int j = 0; j < nf; ++j) pts[j] = dev_fr(point[i + j]), qo[j] = lvl_qoff[i + j];
+            launch_open_fold(rin, rout, q, nf, pts, qo, n >> (i + nf), C.stream);
+        } else {
+            launch_open_level(rin, rout, lvl_qoff[i] != ~0ull ? q + lvl_qoff[i] : q, dev_fr(point[i]), half, C.stream);
+        }
+        rin = rout;
+        i += nf;
+    }
+    for (int i = 0; i < L; ++i) {
+        const uint64_t half = n >> (i + 1);
+        if (i < first) continue;  // the level's proof is proof0
         MsmInst& I = insts[i - first];
         I.pts_off = P.g2_off[i];
         I.stride = (uint32_t)half;
@@ -891,6 +911,13 @@ static std::vector<HFr> sc1_message(const HFr& Cc, const HFr& tau, const HFr g[3
         P[t] = Cc * eq1(tau, T) * Gt;
     }
     return P;
+}
+
+// the quadratic through (0, g0), (1, g1), (2, g2) at t
+static HFr quad_at(const HFr g[3], const HFr& t) {
+    static const HFr inv2 = HFr::from_u64(2).inv();
+    const HFr one = HFr::one(), two = HFr::from_u64(2);
+    return g[0] * ((t - one) * (t - two) * inv2) - g[1] * (t * (t - two)) + g[2] * (t * (t - one) * inv2);
 }
 
 // ====================================================================== prove
@@ -1046,7 +1073,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // ---- sumcheck #1 (lib.rs:86-103)
     proof.u64((uint64_t)L);
     std::vector<HFr> r_x;
-    HFr Cc = HFr::one();
+    HFr Cc = HFr::one(), claim1 = HFr::zero();
     Fr* res_dev = C.pin_dev<Fr>(hp);  // the rounds' sums land in pinned host memory (hp)
     Tables3 cur{{Az, Bz, Cz}};
     const Fr* Ecur = E1;
@@ -1061,8 +1088,13 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             out = Tables3{{fb[0], fb[1], fb[2]}};
             if (i < L - g) Eout = Ebuf[i & 1];
         }
+        // from round 2 on, P_i(0) + P_i(1) = P_{i-1}(r_{i-1}) (the claim) is an identity of the folded
+        // tables, so G(1) follows from G(0): Cc (1 - tau) G(0) + Cc tau G(1) = claim; the kernel skips it
+        // (2 of its 12 Fr products per pair). Exact field arithmetic: the same message bytes.
+        const HFr ct = Cc * tau[i - 1];
+        const bool derive1 = fold && !ct.is_zero();
         launch_sc1_round(fold, cur, out, Ecur, Eout, fold ? dev_fr(r_x[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
-                         C.stream);
+                         !derive1, C.stream);
         C.sync();
         HFr gs[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1071,6 +1103,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             for (int r = 0; r < G; ++r)
                 for (int k = 0; k < 3; ++k) gs[k] += all[3 * r + k];
         }
+        if (derive1) gs[1] = (claim1 - (Cc - ct) * gs[0]) * ct.inv();
         std::vector<HFr> msg = sc1_message(Cc, tau[i - 1], gs, L);
         size_t m0 = proof.b.size();
         proof.u64(msg.size());
@@ -1078,7 +1111,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
         HFr ch = T.rand_fr();
         r_x.push_back(ch);
-        Cc = Cc * eq1(tau[i - 1], ch);
+        const HFr eqc = eq1(tau[i - 1], ch);
+        claim1 = Cc * eqc * quad_at(gs, ch);  // P_i(r_i)
+        Cc = Cc * eqc;
         if (fold) {
             cur = out;
             if (Eout) Ecur = Eout;
@@ -1172,6 +1207,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // ---- sumcheck #2 (lib.rs:114-131)
     proof.u64((uint64_t)L);
     std::vector<HFr> r_y;
+    HFr claim2 = HFr::zero();
     const Fr* Mc = M0;
     const Fr* Zc = zl;
     Fr* Mb[2] = {M1, M2};
@@ -1181,8 +1217,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         const bool fold = i >= 2;
         Fr* Mo = fold ? Mb[i & 1] : nullptr;
         Fr* Zo = fold ? Zb[i & 1] : nullptr;
+        // from round 2 on, P(1) = claim - P(0) (the folded tables' identity): the kernel skips it
         launch_sc2_round(fold, Mc, Zc, Mo, Zo, fold ? dev_fr(r_y[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
-                         C.stream);
+                         !fold, C.stream);
         C.sync();
         HFr ps[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1191,12 +1228,14 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             for (int r = 0; r < G; ++r)
                 for (int k = 0; k < 3; ++k) ps[k] += all[3 * r + k];
         }
+        if (fold) ps[1] = claim2 - ps[0];
         size_t m0 = proof.b.size();
         proof.u64(3);
         for (int k = 0; k < 3; ++k) proof.fr(ps[k]);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);
         HFr ch = T.rand_fr();
         r_y.push_back(ch);
+        claim2 = quad_at(ps, ch);  // P_i(r_i)
         if (fold) {
             Mc = Mo;
             Zc = Zo;

@@ -988,9 +988,15 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // is nothing to hide it behind: it then runs on the context's second stream, beside the commitment
     // and the first opening, and is reused by the second opening. (Both forms give every rank the same
     // batches, so the exchanges of a proof-sharded prove line up.)
+    // SPX_LVL0=batch (A/B; must be the same on every rank of a proof-sharded prove): level 0 inside the
+    // first opening's MSM batch instead, one MSM pipeline (sort, weighting tree) less per proof
+    static const bool lvl0_batch = [] {
+        const char* e = getenv("SPX_LVL0");
+        return e && std::string(e) == "batch";
+    }();
     const bool share0 = !o.stub;
-    const bool early0 = share0 && !(o.cached && I.has_cache);
-    const bool side0 = share0 && !early0;
+    const bool early0 = share0 && !lvl0_batch && !(o.cached && I.has_cache);
+    const bool side0 = share0 && !lvl0_batch && !early0;
     const MsmShard sh = shard_of(comm);
     if (side0) {  // z is in place: the second stream may start
         C.ensure_side();
@@ -1044,8 +1050,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     std::vector<HFr> pt1(L, HFr::zero());
     for (int i = 0; i < log_v; ++i) pt1[i] = T.rand_fr();
     {
-        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G) : open_z(C, *P, z, L, pt1, comm, share0 ? &proof0 : nullptr);
+        OpenOut op = o.stub ? open_stub(C, zl, L, pt1, G)
+                            : open_z(C, *P, z, L, pt1, comm, (early0 || side0) ? &proof0 : nullptr);
         if (side0) op.proofs[0] = proof0 = lvl0_finish(C, *P, z, L, comm, true);
+        if (share0 && !early0 && !side0) proof0 = op.proofs[0];
         size_t m0 = proof.b.size();
         ser_open(proof, op.eval, h_of(P), op.proofs);
         T.feed(proof.b.data() + m0, proof.b.size() - m0);

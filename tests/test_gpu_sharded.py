@@ -88,3 +88,23 @@ def test_virtual_ranks_crowded_buckets(spx, oc, fill):
     assert all(p == want for p in out)
     if fill == _ONES7:
         assert reruns > 0, "crowded scalars did not overflow rank 0's keys"
+
+
+def test_rehearsal_rank_runs(spx, oc):
+    """spx_ctx_set_comm_rehearsal: one rank of a G-rank proof-sharded prove without peers (bench.py's node
+    rehearsal). Its proofs are not valid; it must run the rank's whole path (compacted keys of its
+    buckets included) and return a proof of the right size, and G = 1 must give the real proof."""
+    log_n, log_v = 10, 3
+    inst = oc.Instance(0, log_n, log_v, 970 + log_n, 0)
+    ppb = oc.PP.keygen(log_n, 971).serialize()
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
+    for G in (1, 4):
+        ctx = spx.Context(0)
+        ctx.set_comm_rehearsal(0, G)
+        pp = spx.PublicParameter.load(ctx, ppb)
+        mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
+        pk = spx.MLArgumentForR1CS.index(ctx, *mats)
+        got = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+        assert len(got) == len(want)
+        assert (got == want) == (G == 1)
+        assert ctx.msm_reruns() == 0

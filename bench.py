@@ -19,11 +19,12 @@ absorption of the matrices (~150 MB per proof, one pool of hashing threads per r
 proofs' GPU work. value = constraints proved per second over the timed region (whole job).
 Beside it: single-proof latency (with and without the index-cached transcript), the index-cached
 throughput, BASELINE config C2 (2^18, sumcheck-only, commitment stubbed) with its own HBM roofline,
-and CPU baselines (test oracle: 1 core at 2^14, all cores at --cpu-all-log-n).
+and CPU baselines (test oracle: 1 core at --cpu-log-n, all cores at --cpu-all-log-n).
 
 N > 1: one process per GPU (torch.distributed.run). Default (--shard proof): every proof is split
 over all ranks (hypercube blocks, per-round partials exchanged by an on-node
-shared-memory allgather, one communicator per proof in flight; --comm rccl uses RCCL). Total work
+shared-memory allgather, one communicator per proof in flight; --comm rccl: one RCCL communicator per rank, shared by the
+proofs in flight through the ordered exchange hub). Total work
 per step is fixed ("scaling": "strong"). --shard batch makes every rank prove its own P proofs
 ("weak"); the other mode's value is reported beside the headline.
 
@@ -374,7 +375,8 @@ def main():
     ap.add_argument("--rehearse", default="2,4,8",
                     help="N = 1: world sizes G for the one-rank rehearsal of a G-GPU proof-sharded node ('' to skip)")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
-                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (needs --inflight 1)")
+                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (one communicator per rank "
+                    "shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm)")
     ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts)")
     ap.add_argument("--proofs-per-step", type=int, default=64,
                     help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
@@ -382,11 +384,6 @@ def main():
     stub = args.config == "c2"
     log_n = args.log_n or (18 if stub else 20)
     log_v = args.log_v
-    if args.comm == "rccl" and args.inflight != 1:
-        # one RCCL communicator per proof in flight, driven by independent threads: their device
-        # collectives can reach shared hardware queues in different orders on different ranks (deadlock)
-        raise SystemExit("--comm rccl needs --inflight 1 (see INTEGRATION.md)")
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -425,10 +422,14 @@ def main():
     def make_sharded(k):
         cs = [spx.Context(device) for _ in range(k)]
         if args.comm == "rccl":
-            uid = [[spx.comm_unique_id() for _ in range(k)] if rank == 0 else None]
+            # ONE communicator per rank; every proof in flight exchanges through its own channel of
+            # the ordered hub (comm_hub.cpp), context j on channel j on every rank
+            uid = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
+            hub = spx.ExchangeHub.rccl(uid[0], rank, world, device)
             for j, c in enumerate(cs):
-                c.set_comm_rccl(uid[0][j], rank, world)
+                c.set_comm_hub(hub, j)
+            hub.close()  # the contexts keep it alive
         else:
             name = [spx.shm_name() if rank == 0 else None]
             dist.broadcast_object_list(name, src=0)

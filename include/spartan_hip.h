@@ -75,9 +75,27 @@ const char *spx_version(void);
 int spx_ctx_create(int device, spx_ctx **out);
 int spx_ctx_destroy(spx_ctx *ctx);
 /* RCCL (one process per GPU): rank 0 calls spx_comm_unique_id, broadcasts the 128 bytes out of band
- * (e.g. torch.distributed), then every rank calls spx_ctx_set_comm_rccl. */
+ * (e.g. torch.distributed), then every rank creates ONE hub on it (spx_comm_hub_create_rccl) and
+ * attaches each of its contexts to a channel (spx_ctx_set_comm_hub): context j of every rank on
+ * channel j (0..63). The hub's thread is the only caller of the communicator and matches the
+ * channels' exchanges across ranks in rounds every rank runs identically, so any number of proofs in
+ * flight share one communicator without collective-ordering deadlocks.
+ * spx_ctx_set_comm_rccl is the one-context shorthand (a private hub, channel 0).
+ * Replaces the reference's single-threaded prove (/root/reference/src/lib.rs:58-146), which has
+ * no exchange; the exchange schedule is DESIGN.md §6. */
 int spx_comm_unique_id(uint8_t id_out[128]);
 int spx_ctx_set_comm_rccl(spx_ctx *ctx, const uint8_t id[128], int rank, int world);
+int spx_comm_hub_create_rccl(const uint8_t id[128], int rank, int world, int device, void **hub_out);
+/* the same hub over the shared-memory transport (one segment per rank set instead of one per
+ * context), and over the in-process test group (virtual ranks as host threads; spx_comm_group_create) */
+int spx_comm_hub_create_shm(const char *name, int rank, int world, void **hub_out);
+int spx_comm_hub_create_group(void *group, int rank, void **hub_out);
+int spx_ctx_set_comm_hub(spx_ctx *ctx, void *hub, int channel);
+/* one exchange on `channel` without a context (transport tests); blocks until every rank posted it */
+int spx_comm_hub_allgather(void *hub, int channel, const void *send, void *recv, size_t bytes);
+/* out[0] control rounds, out[1] data rounds, out[2] exchanges served, out[3] largest batch per round */
+int spx_comm_hub_stats(void *hub, uint64_t out[4]);
+int spx_comm_hub_destroy(void *hub); /* contexts attached keep the hub alive until they are destroyed */
 /* On-node shared-memory communicator (default for one process per GPU on one host): every rank
  * passes the same `name` (rank 0 makes it unique, e.g. "spx_<random hex>_<k>", and distributes it
  * out of band), one name per context. The exchanges of a sharded proof are host-side and tiny, so

@@ -83,6 +83,13 @@ EXPORTED = [
     "spx_comm_group_destroy",
     "spx_ctx_set_comm_group",
     "spx_ctx_set_comm_rehearsal",
+    "spx_comm_hub_create_rccl",
+    "spx_comm_hub_create_shm",
+    "spx_comm_hub_create_group",
+    "spx_ctx_set_comm_hub",
+    "spx_comm_hub_allgather",
+    "spx_comm_hub_stats",
+    "spx_comm_hub_destroy",
     "spx_ctx_comm_allgather",
     "spx_pp_load",
     "spx_pp_generate",
@@ -145,6 +152,13 @@ def lib():
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
     L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    L.spx_comm_hub_create_rccl.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_comm_hub_create_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_comm_hub_create_group.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.spx_ctx_set_comm_hub.argtypes = [vp, vp, ctypes.c_int]
+    L.spx_comm_hub_allgather.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p, sz]
+    L.spx_comm_hub_stats.argtypes = [vp, ctypes.c_void_p]
+    L.spx_comm_hub_destroy.argtypes = [vp]
     L.spx_ctx_comm_allgather.argtypes = [vp, ctypes.c_char_p, ctypes.c_void_p, sz]
     L.spx_pp_load.argtypes = [vp, u8p, sz, ctypes.POINTER(vp)]
     L.spx_pp_generate.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
@@ -267,6 +281,10 @@ class Context:
     def set_comm_group(self, group, rank):
         _check(lib().spx_ctx_set_comm_group(self.h, group.h, int(rank)))
 
+    def set_comm_hub(self, hub, channel):
+        """exchanges through channel `channel` of an ExchangeHub (context j of every rank on channel j)"""
+        _check(lib().spx_ctx_set_comm_hub(self.h, hub.h, int(channel)))
+
     def set_comm_rehearsal(self, rank, world):
         """one rank of a world-rank proof-sharded prove without its peers (throughput rehearsal; the
         proofs are not valid)"""
@@ -299,7 +317,7 @@ class CommGroup:
     def __init__(self, world):
         h = ctypes.c_void_p()
         _check(lib().spx_comm_group_create(int(world), ctypes.byref(h)))
-        self.h = h
+        self.h, self.world = h, int(world)
 
     def __del__(self):
         try:
@@ -326,6 +344,56 @@ class ShmComm:
     def close(self):
         if self.h:
             lib().spx_comm_shm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ExchangeHub:
+    """One collective transport per rank shared by every proof in flight, ordered by channel
+    (comm_hub.cpp): ExchangeHub.rccl(uid, rank, world, device), .shm(name, rank, world) or
+    .group(CommGroup, rank)."""
+
+    def __init__(self, h, world):
+        self.h, self.world = h, int(world)
+
+    @classmethod
+    def rccl(cls, unique_id, rank, world, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_hub_create_rccl(bytes(unique_id), int(rank), int(world), int(device), ctypes.byref(h)))
+        return cls(h, world)
+
+    @classmethod
+    def shm(cls, name, rank, world):
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_hub_create_shm(name.encode(), int(rank), int(world), ctypes.byref(h)))
+        return cls(h, world)
+
+    @classmethod
+    def group(cls, group, rank):
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_hub_create_group(group.h, int(rank), ctypes.byref(h)))
+        return cls(h, group.world)
+
+    def allgather(self, channel, data):
+        data = bytes(data)
+        out = ctypes.create_string_buffer(max(1, len(data) * self.world))
+        _check(lib().spx_comm_hub_allgather(self.h, int(channel), data, out, len(data)))
+        return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(self.world)]
+
+    def stats(self):
+        """control rounds, data rounds, exchanges served, largest batch in one round"""
+        out = (ctypes.c_uint64 * 4)()
+        _check(lib().spx_comm_hub_stats(self.h, out))
+        return dict(zip(("rounds", "data_rounds", "served", "max_batch"), list(out)))
+
+    def close(self):
+        if self.h:
+            lib().spx_comm_hub_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -123,7 +123,8 @@ int spx_ctx_set_comm_rccl(spx_ctx* ctx, const uint8_t id[128], int rank, int wor
     return guard([&] {
         set_dev(ctx);
         if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
-        ctx->c->comm = spx::make_rccl_comm(id, rank, world, ctx->c->device, ctx->c->stream);
+        // a private hub on channel 0: the same ordered path as spx_comm_hub_create_rccl
+        ctx->c->comm = spx::make_hub_channel(spx::make_hub(spx::make_rccl_comm(id, rank, world, ctx->c->device, nullptr)), 0);
     });
 }
 int spx_ctx_set_comm_shm(spx_ctx* ctx, const char* name, int rank, int world) {
@@ -161,6 +162,50 @@ int spx_ctx_set_comm_group(spx_ctx* ctx, void* group, int rank) {
         auto& st = *static_cast<std::shared_ptr<spx::GroupState>*>(group);
         if (rank < 0 || rank >= st->world) spx::invalid("bad rank");
         ctx->c->comm.reset(new spx::GroupComm(st, rank));
+    });
+}
+
+// ordered exchange hubs: a handle owns a shared_ptr; contexts attached to it keep it alive
+int spx_comm_hub_create_rccl(const uint8_t id[128], int rank, int world, int device, void** hub_out) {
+    return guard([&] {
+        if (!hub_out || !id) spx::invalid("null argument");
+        if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
+        *hub_out = new std::shared_ptr<spx::OrderedHub>(spx::make_hub(spx::make_rccl_comm(id, rank, world, device, nullptr)));
+    });
+}
+int spx_comm_hub_create_shm(const char* name, int rank, int world, void** hub_out) {
+    return guard([&] {
+        if (!hub_out) spx::invalid("null output");
+        *hub_out = new std::shared_ptr<spx::OrderedHub>(spx::make_hub(spx::make_shm_comm(name, rank, world)));
+    });
+}
+int spx_comm_hub_create_group(void* group, int rank, void** hub_out) {
+    return guard([&] {
+        if (!hub_out || !group) spx::invalid("null argument");
+        auto& st = *static_cast<std::shared_ptr<spx::GroupState>*>(group);
+        if (rank < 0 || rank >= st->world) spx::invalid("bad rank");
+        *hub_out = new std::shared_ptr<spx::OrderedHub>(spx::make_hub(std::unique_ptr<spx::Comm>(new spx::GroupComm(st, rank))));
+    });
+}
+int spx_comm_hub_allgather(void* hub, int channel, const void* send, void* recv, size_t bytes) {
+    return guard([&] {
+        if (!hub || (bytes && (!send || !recv))) spx::invalid("null argument");
+        spx::hub_allgather(**static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), channel, send, recv, bytes);
+    });
+}
+int spx_comm_hub_stats(void* hub, uint64_t out[4]) {
+    return guard([&] {
+        if (!hub || !out) spx::invalid("null argument");
+        spx::hub_stats(**static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), out);
+    });
+}
+int spx_comm_hub_destroy(void* hub) {
+    return guard([&] { delete static_cast<std::shared_ptr<spx::OrderedHub>*>(hub); });
+}
+int spx_ctx_set_comm_hub(spx_ctx* ctx, void* hub, int channel) {
+    return guard([&] {
+        if (!ctx || !hub) spx::invalid("null argument");
+        ctx->c->comm = spx::make_hub_channel(*static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), channel);
     });
 }
 

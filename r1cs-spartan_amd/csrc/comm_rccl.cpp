@@ -17,17 +17,17 @@ namespace spx {
 
 // The exchange runs on the communicator's OWN stream, with pinned staging: the host waits only for
 // the collective, never for the proof's queued kernels (the commitment MSM keeps running while the
-// transcript state is exchanged). One communicator drives one proof at a time (see INTEGRATION.md:
-// several communicators driven by independent threads can order their collectives differently on
-// different ranks).
+// transcript state is exchanged). Several proofs in flight share ONE communicator through the
+// ordered exchange hub (comm_hub.cpp): independent communicators driven by independent threads
+// could order their collectives differently on different ranks.
 struct RcclComm : Comm {
     ncclComm_t comm = nullptr;
-    int r, w;
+    int r, w, dev;
     hipStream_t s = nullptr;
     DevMem sbuf, rbuf;
     uint8_t *hs = nullptr, *hr = nullptr;
     size_t hcap = 0;
-    RcclComm(const uint8_t id[128], int rank, int world) : r(rank), w(world) {
+    RcclComm(const uint8_t id[128], int rank, int world, int device) : r(rank), w(world), dev(device) {
         ncclUniqueId uid;
         static_assert(sizeof(uid) == 128, "ncclUniqueId size");
         memcpy(&uid, id, 128);
@@ -43,6 +43,7 @@ struct RcclComm : Comm {
     int rank() const override { return r; }
     int size() const override { return w; }
     void allgather(const void* send, void* recv, size_t bytes) override {
+        SPX_HIP(hipSetDevice(dev));  // the calling thread may be an exchange hub's (device 0 by default)
         if (bytes * w > hcap) {  // grow only between calls: the previous call synchronised s
             if (hs) SPX_HIP(hipHostFree(hs));
             if (hr) SPX_HIP(hipHostFree(hr));
@@ -64,7 +65,7 @@ struct RcclComm : Comm {
 
 std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int rank, int world, int device, hipStream_t) {
     SPX_HIP(hipSetDevice(device));
-    return std::unique_ptr<Comm>(new RcclComm(id, rank, world));
+    return std::unique_ptr<Comm>(new RcclComm(id, rank, world, device));
 }
 
 }  // namespace spx

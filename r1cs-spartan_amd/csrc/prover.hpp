@@ -129,6 +129,13 @@ struct GroupComm : Comm {
 };
 std::unique_ptr<Comm> make_shm_comm(const char* name, int rank, int world);
 std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int rank, int world, int device, hipStream_t s);
+// ordered exchange hub (comm_hub.cpp): one transport per process shared by many proofs in flight,
+// each context on its own channel (0..63)
+struct OrderedHub;
+std::shared_ptr<OrderedHub> make_hub(std::unique_ptr<Comm> base);
+std::unique_ptr<Comm> make_hub_channel(const std::shared_ptr<OrderedHub>& hub, int channel);
+void hub_allgather(OrderedHub& hub, int channel, const void* send, void* recv, size_t bytes);
+void hub_stats(OrderedHub& hub, uint64_t out[4]);  // rounds, data rounds, exchanges served, largest batch
 
 // ---------------------------------------------------------------- context
 struct Ctx {

@@ -4,6 +4,7 @@ import argparse
 import importlib.util
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -35,9 +36,43 @@ def allgather_check(spx, name, rank, world, out):
     open(out, "w").write("ok %s" % res)
 
 
+def hub_payload(rank, ch, i):
+    size = (ch * 37 + i * 11) % 300  # sizes differ per (channel, exchange), agree across ranks
+    return bytes(((rank * 89 + ch * 13 + i * 7 + j) & 0xFF) for j in range(size))
+
+
+def hub_check(spx, hub, rank, world, channels, iters, seed):
+    """`channels` threads on this rank, each a fixed sequence of `iters` exchanges on its channel,
+    with random pauses so the ranks reach the channels in different orders."""
+    import random
+    import threading
+
+    errs = []
+
+    def worker(ch):
+        rng = random.Random(seed * 1000 + rank * 100 + ch)
+        try:
+            for i in range(iters):
+                if rng.random() < 0.3:
+                    time.sleep(rng.random() * 0.002)
+                got = hub.allgather(ch, hub_payload(rank, ch, i))
+                if got != [hub_payload(k, ch, i) for k in range(world)]:
+                    errs.append("mismatch ch %d exchange %d" % (ch, i))
+                    return
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(ch,)) for ch in range(channels)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return errs
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["allgather", "prove"], required=True)
+    ap.add_argument("--mode", choices=["allgather", "hub", "prove", "prove_hub"], required=True)
     ap.add_argument("--name", required=True)
     ap.add_argument("--rank", type=int, required=True)
     ap.add_argument("--world", type=int, required=True)
@@ -50,12 +85,23 @@ def main():
     if a.mode == "allgather":
         allgather_check(spx, a.name, a.rank, a.world, a.out)
         return
+    if a.mode == "hub":
+        hub = spx.ExchangeHub.shm(a.name, a.rank, a.world)
+        errs = hub_check(spx, hub, a.rank, a.world, 8, 60, 5)
+        st = hub.stats()
+        hub.close()
+        open(a.out, "w").write(("ok %s" % st) if not errs else "fail %s" % errs[:3])
+        return
     sys.path.insert(0, ROOT)
     import bench
 
     ctxs = [spx.Context(0) for _ in range(a.inflight)]
+    hub = spx.ExchangeHub.shm(a.name, a.rank, a.world) if a.mode == "prove_hub" else None
     for k, c in enumerate(ctxs):
-        c.set_comm_shm("%s_%d" % (a.name, k), a.rank, a.world)
+        if hub is not None:
+            c.set_comm_hub(hub, k)  # every proof in flight through the one ordered transport
+        else:
+            c.set_comm_shm("%s_%d" % (a.name, k), a.rank, a.world)
     syn, mats, z, nnz = bench.synth_one(spx, 0, a.log_n, a.log_v, 0x5EED0000 + a.log_n)
     pp = spx.MLProofForR1CS.setup(ctxs[0], a.log_n, 77)
     pk = spx.IndexPK(ctxs[0], bench.index_from_c(spx, ctxs[0], mats), a.log_n)

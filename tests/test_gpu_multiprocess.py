@@ -1,6 +1,7 @@
 """Sharded proof across real processes on the GPU box: 2 ranks (both on GPU 0), each with 2 proofs
 in flight over shared-memory communicators, exactly the bench's N > 1 structure. Every proof of
-both ranks must equal the oracle's unsharded proof byte for byte."""
+both ranks must equal the oracle's unsharded proof byte for byte. The hub case shares one transport
+per rank among 4 proofs in flight."""
 import os
 
 import pytest
@@ -19,15 +20,18 @@ def _read(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("log_n", [8, 11])
-def test_sharded_processes_bit_exact(spx, oc, log_n):
+@pytest.mark.parametrize("log_n,mode,inflight", [(8, "prove", 2), (11, "prove", 2), (10, "prove_hub", 4)])
+def test_sharded_processes_bit_exact(spx, oc, log_n, mode, inflight):
+    """mode prove_hub: all proofs in flight of a rank share ONE transport through the ordered exchange
+    hub (comm_hub.cpp, the structure of bench.py --comm rccl), here over shared memory"""
     log_v = 3
-    outs = _run_workers(spx, 2, "prove", ["--log-n", str(log_n), "--log-v", str(log_v), "--inflight", "2"], timeout=300)
+    outs = _run_workers(spx, 2, mode, ["--log-n", str(log_n), "--log-v", str(log_v), "--inflight", str(inflight)],
+                        timeout=300)
     per_rank = [_read(o) for o in outs]
     for o in outs:
         os.remove(o)
     proofs = [p for items in per_rank for p in items[:-1]]
-    assert len(proofs) == 8
+    assert len(proofs) == 2 * 2 * inflight
     inst = oc.Instance(0, log_n, log_v, 0x5EED0000 + log_n)
     ppc = oc.PP.keygen(log_n, 77)
     assert per_rank[0][-1] == ppc.serialize()

@@ -152,13 +152,14 @@ def lib():
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
     L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
-    L.spx_comm_hub_create_rccl.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
-    L.spx_comm_hub_create_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
-    L.spx_comm_hub_create_group.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
-    L.spx_ctx_set_comm_hub.argtypes = [vp, vp, ctypes.c_int]
-    L.spx_comm_hub_allgather.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p, sz]
-    L.spx_comm_hub_stats.argtypes = [vp, ctypes.c_void_p]
-    L.spx_comm_hub_destroy.argtypes = [vp]
+    if hasattr(L, "spx_comm_hub_create_rccl") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate the hub
+        L.spx_comm_hub_create_rccl.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.spx_comm_hub_create_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.spx_comm_hub_create_group.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+        L.spx_ctx_set_comm_hub.argtypes = [vp, vp, ctypes.c_int]
+        L.spx_comm_hub_allgather.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p, sz]
+        L.spx_comm_hub_stats.argtypes = [vp, ctypes.c_void_p]
+        L.spx_comm_hub_destroy.argtypes = [vp]
     L.spx_ctx_comm_allgather.argtypes = [vp, ctypes.c_char_p, ctypes.c_void_p, sz]
     L.spx_pp_load.argtypes = [vp, u8p, sz, ctypes.POINTER(vp)]
     L.spx_pp_generate.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
@@ -195,6 +196,8 @@ def lib():
     L.spx_open.argtypes = [vp, vp, u8p, ctypes.c_int, u8p, ctypes.c_void_p, ctypes.c_void_p]
     for name in EXPORTED:
         if name not in ("spx_last_error", "spx_version", "spx_proof_size"):
+            if os.environ.get("SPX_LIB_PATH") and not hasattr(L, name):
+                continue  # an older A/B build (tools/ab_bench.sh); the in-tree library must export all
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

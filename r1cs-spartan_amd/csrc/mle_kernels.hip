@@ -27,6 +27,20 @@ DEV Fr ld_fr(const Fr* p) {
     return r;
 }
 DEV void st_fr(Fr* p, const Fr& v) { store_vec(p, v); }
+// folded sumcheck tables: written once, read by the next round (SPX_FOLD_NT=1: non-temporal stores)
+#ifndef SPX_FOLD_NT
+#define SPX_FOLD_NT 0
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+DEV void st_fr_fold(Fr* p, const Fr& v) {
+    if constexpr (SPX_FOLD_NT) {
+        u32x4* d = reinterpret_cast<u32x4*>(p);
+        __builtin_nontemporal_store((u32x4){v.v[0], v.v[1], v.v[2], v.v[3]}, d);
+        __builtin_nontemporal_store((u32x4){v.v[4], v.v[5], v.v[6], v.v[7]}, d + 1);
+    } else {
+        store_vec(p, v);
+    }
+}
 
 // ------------------------------------------------------------------ block reduction of K Fr values
 template <int K>
@@ -304,31 +318,40 @@ __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out,
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
-        Fr x0[3], x1[3];
+        Fr x0[3], x1[3], e;
+        if (FOLD) {
+            // every load of the pair is issued before the first store (the in/out tables may not alias,
+            // but the compiler cannot know): one memory round trip per element instead of four
+            Fr a[3][4], e0, e1;
 #pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            if (FOLD) {
-                Fr a0 = ld_fr(in.t[m] + 4 * b), a1 = ld_fr(in.t[m] + 4 * b + 1);
-                Fr a2 = ld_fr(in.t[m] + 4 * b + 2), a3 = ld_fr(in.t[m] + 4 * b + 3), d;
-                fe_sub(d, a1, a0);
+            for (int m = 0; m < 3; ++m)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a[m][k] = ld_fr(in.t[m] + 4 * b + k);
+            e0 = ld_fr(Ein + 2 * b);
+            e1 = ld_fr(Ein + 2 * b + 1);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                Fr d;
+                fe_sub(d, a[m][1], a[m][0]);
                 fe_mul(d, d, r);
-                fe_add(x0[m], a0, d);
-                fe_sub(d, a3, a2);
+                fe_add(x0[m], a[m][0], d);
+                fe_sub(d, a[m][3], a[m][2]);
                 fe_mul(d, d, r);
-                fe_add(x1[m], a2, d);
-                st_fr(out.t[m] + 2 * b, x0[m]);
-                st_fr(out.t[m] + 2 * b + 1, x1[m]);
-            } else {
+                fe_add(x1[m], a[m][2], d);
+            }
+            fe_add(e, e0, e1);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                st_fr_fold(out.t[m] + 2 * b, x0[m]);
+                st_fr_fold(out.t[m] + 2 * b + 1, x1[m]);
+            }
+            if (Eout) st_fr_fold(Eout + b, e);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
                 x0[m] = ld_fr(in.t[m] + 2 * b);
                 x1[m] = ld_fr(in.t[m] + 2 * b + 1);
             }
-        }
-        Fr e;
-        if (FOLD) {
-            Fr e0 = ld_fr(Ein + 2 * b), e1 = ld_fr(Ein + 2 * b + 1);
-            fe_add(e, e0, e1);
-            if (Eout) st_fr(Eout + b, e);
-        } else {
             e = ld_fr(Ein + b);
         }
         Fr t, u;
@@ -376,25 +399,28 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr m0, m1, z0, z1;
         if (FOLD) {
-            Fr d;
-            Fr a0 = ld_fr(Min + 4 * b), a1 = ld_fr(Min + 4 * b + 1), a2 = ld_fr(Min + 4 * b + 2), a3 = ld_fr(Min + 4 * b + 3);
-            fe_sub(d, a1, a0);
+            Fr d, a[4], c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[k] = ld_fr(Min + 4 * b + k);
+                c[k] = ld_fr(Zin + 4 * b + k);
+            }
+            fe_sub(d, a[1], a[0]);
             fe_mul(d, d, r);
-            fe_add(m0, a0, d);
-            fe_sub(d, a3, a2);
+            fe_add(m0, a[0], d);
+            fe_sub(d, a[3], a[2]);
             fe_mul(d, d, r);
-            fe_add(m1, a2, d);
-            Fr c0 = ld_fr(Zin + 4 * b), c1 = ld_fr(Zin + 4 * b + 1), c2 = ld_fr(Zin + 4 * b + 2), c3 = ld_fr(Zin + 4 * b + 3);
-            fe_sub(d, c1, c0);
+            fe_add(m1, a[2], d);
+            fe_sub(d, c[1], c[0]);
             fe_mul(d, d, r);
-            fe_add(z0, c0, d);
-            fe_sub(d, c3, c2);
+            fe_add(z0, c[0], d);
+            fe_sub(d, c[3], c[2]);
             fe_mul(d, d, r);
-            fe_add(z1, c2, d);
-            st_fr(Mout + 2 * b, m0);
-            st_fr(Mout + 2 * b + 1, m1);
-            st_fr(Zout + 2 * b, z0);
-            st_fr(Zout + 2 * b + 1, z1);
+            fe_add(z1, c[2], d);
+            st_fr_fold(Mout + 2 * b, m0);
+            st_fr_fold(Mout + 2 * b + 1, m1);
+            st_fr_fold(Zout + 2 * b, z0);
+            st_fr_fold(Zout + 2 * b + 1, z1);
         } else {
             m0 = ld_fr(Min + 2 * b);
             m1 = ld_fr(Min + 2 * b + 1);

@@ -11,7 +11,8 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 proofs = float(sys.argv[2])
 ghz = float(sys.argv[3]) if len(sys.argv) > 3 else 2.4
-SETUP = ("k_precompute", "k_fixed_base", "k_normalize", "k_aff_to_r29", "k_points_from_bytes", "k_points_to_canon")
+SETUP = ("k_precompute", "k_fixed_base", "k_normalize", "k_aff_to_r29", "k_points_from_bytes", "k_points_to_canon",
+         "__amd_rocclr")  # the last: PP window-copy blits (hipMemcpy2DAsync, prover.cpp pp_preprocess)
 acc = defaultdict(lambda: defaultdict(float))
 for r in rows:
     name = re.sub(r"\(.*", "", r["Kernel_Name"])

@@ -96,8 +96,24 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
             if (hist && key != ~0u) atomicAdd(&hist[key], 1u);
         }
     } else {
-        uint32_t cnt = 0;
-        if (live) {
+        // the digits are extracted once: for up to kKeep windows (c >= 16 at the sizes that matter) the
+        // counting pass keeps every window's key and reference in registers (the window loop unrolled,
+        // so the arrays are indexed statically); more windows recompute them in the writing pass
+        constexpr uint32_t kKeep = 16;
+        uint32_t cnt = 0, kkey[kKeep], kref[kKeep];
+        if (live && I.W <= kKeep) {
+            Digits d = d0;
+#pragma unroll
+            for (uint32_t w = 0; w < kKeep; ++w) {
+                kkey[w] = ~0u;
+                if (w < I.W) {
+                    const int32_t dg = d.next(I.c);
+                    kkey[w] = digit_key(I, dg);
+                    kref[w] = digit_ref(I, w, j, dg);
+                }
+                cnt += kkey[w] != ~0u;
+            }
+        } else if (live) {
             Digits d = d0;
             for (uint32_t w = 0; w < I.W; ++w) cnt += digit_key(I, d.next(I.c)) != ~0u;
         }
@@ -112,7 +128,19 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
             if ((uint64_t)base + agg > cap) atomicOr(&st[0], kMsmOverflow);
         }
         __syncthreads();
-        if (cnt) {
+        if (cnt && I.W <= kKeep) {
+            uint64_t pos = (uint64_t)base + pre;
+#pragma unroll
+            for (uint32_t w = 0; w < kKeep; ++w)
+                if (kkey[w] != ~0u) {
+                    if (pos < cap) {
+                        keys[pos] = kkey[w];
+                        vals[pos] = kref[w];
+                        if (hist) atomicAdd(&hist[kkey[w]], 1u);
+                    }
+                    ++pos;
+                }
+        } else if (cnt) {
             uint64_t pos = (uint64_t)base + pre;
             Digits d = d0;
             for (uint32_t w = 0; w < I.W; ++w) {

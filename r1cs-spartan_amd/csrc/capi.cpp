@@ -124,13 +124,13 @@ int spx_ctx_set_comm_rccl(spx_ctx* ctx, const uint8_t id[128], int rank, int wor
         set_dev(ctx);
         if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
         // a private hub on channel 0: the same ordered path as spx_comm_hub_create_rccl
-        ctx->c->comm = spx::make_hub_channel(spx::make_hub(spx::make_rccl_comm(id, rank, world, ctx->c->device, nullptr)), 0);
+        ctx->c->set_comm(spx::make_hub_channel(spx::make_hub(spx::make_rccl_comm(id, rank, world, ctx->c->device, nullptr)), 0));
     });
 }
 int spx_ctx_set_comm_shm(spx_ctx* ctx, const char* name, int rank, int world) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");
-        ctx->c->comm = spx::make_shm_comm(name, rank, world);
+        ctx->c->set_comm(spx::make_shm_comm(name, rank, world));
     });
 }
 int spx_comm_shm_create(const char* name, int rank, int world, void** comm_out) {
@@ -161,7 +161,7 @@ int spx_ctx_set_comm_group(spx_ctx* ctx, void* group, int rank) {
     return guard([&] {
         auto& st = *static_cast<std::shared_ptr<spx::GroupState>*>(group);
         if (rank < 0 || rank >= st->world) spx::invalid("bad rank");
-        ctx->c->comm.reset(new spx::GroupComm(st, rank));
+        ctx->c->set_comm(std::unique_ptr<spx::Comm>(new spx::GroupComm(st, rank)));
     });
 }
 
@@ -205,7 +205,7 @@ int spx_comm_hub_destroy(void* hub) {
 int spx_ctx_set_comm_hub(spx_ctx* ctx, void* hub, int channel) {
     return guard([&] {
         if (!ctx || !hub) spx::invalid("null argument");
-        ctx->c->comm = spx::make_hub_channel(*static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), channel);
+        ctx->c->set_comm(spx::make_hub_channel(*static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), channel));
     });
 }
 
@@ -213,7 +213,7 @@ int spx_ctx_set_comm_rehearsal(spx_ctx* ctx, int rank, int world) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");
         if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
-        ctx->c->comm.reset(new spx::SoloComm(rank, world));
+        ctx->c->set_comm(std::unique_ptr<spx::Comm>(new spx::SoloComm(rank, world)));
     });
 }
 

@@ -922,6 +922,20 @@ static HFr quad_at(const HFr g[3], const HFr& t) {
 
 // ====================================================================== prove
 std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts& o) {
+    // A prove that throws may leave work queued on both streams that still reads W.z and writes the
+    // context's slots: drain them while unwinding, so the caller may free the witness and the next
+    // proof on this context starts from idle streams.
+    struct UnwindDrain {
+        Ctx& C;
+        int pending = std::uncaught_exceptions();
+        ~UnwindDrain() {
+            if (std::uncaught_exceptions() <= pending) return;
+            (void)hipStreamSynchronize(C.stream);
+            if (C.side) (void)hipStreamSynchronize(C.side);
+            msm_ws_staging_reset(C.msm);
+            if (C.msm_side) msm_ws_staging_reset(C.msm_side);
+        }
+    } drain{C};
     Timer tall;
     C.timings.clear();
     auto mark = [&](const char* name, Timer& t) {
@@ -994,6 +1008,16 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         const char* e = getenv("SPX_LVL0");
         return e && std::string(e) == "batch";
     }();
+    if (G > 1 && !C.knobs_agreed) {
+        // the level-0 mode decides the order and sizes of a proof's exchanges: every rank of the
+        // communicator must read the same SPX_LVL0 (one exchange on a context's first sharded proof)
+        const uint32_t mine = lvl0_batch ? 1u : 0u;
+        std::vector<uint32_t> all(G);
+        comm.allgather(&mine, all.data(), sizeof mine);
+        for (int r = 0; r < G; ++r)
+            if (all[r] != mine) invalid("SPX_LVL0 differs between the ranks of this communicator");
+        C.knobs_agreed = true;
+    }
     const bool share0 = !o.stub;
     const bool early0 = share0 && !lvl0_batch && !(o.cached && I.has_cache);
     const bool side0 = share0 && !lvl0_batch && !early0;

@@ -149,6 +149,10 @@ struct Ctx {
     hipEvent_t side_ev = nullptr;
     void ensure_side();
     std::unique_ptr<Comm> comm;
+    void set_comm(std::unique_ptr<Comm> c) {
+        comm = std::move(c);
+        knobs_agreed = false;
+    }
     // Pinned host staging, one fixed carve-out per context (allocated once, never moved: a region a
     // caller holds stays valid while its async copies run). Every region is reused only after a
     // stream sync that covers the copies issued from it.
@@ -180,6 +184,7 @@ struct Ctx {
     std::vector<std::pair<std::string, double>> timings;
     KProf kprof;
     uint64_t prove_seq = 0;  // proofs started on this context (identical on every rank of its communicator)
+    bool knobs_agreed = false;  // exchange-shaping env knobs checked equal across the communicator
     std::atomic<uint64_t> msm_reruns{0};  // MSM batches rerun dense after a compacted-key overflow
     Ctx(int dev);
     ~Ctx();

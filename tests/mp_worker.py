@@ -72,7 +72,7 @@ def hub_check(spx, hub, rank, world, channels, iters, seed):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["allgather", "hub", "prove", "prove_hub"], required=True)
+    ap.add_argument("--mode", choices=["allgather", "hub", "prove", "prove_hub", "lvl0_mismatch"], required=True)
     ap.add_argument("--name", required=True)
     ap.add_argument("--rank", type=int, required=True)
     ap.add_argument("--world", type=int, required=True)
@@ -95,6 +95,23 @@ def main():
     sys.path.insert(0, ROOT)
     import bench
 
+    if a.mode == "lvl0_mismatch":
+        # rank 1 alone reads SPX_LVL0=batch: the ranks' first sharded proof must refuse to run
+        if a.rank == 1:
+            os.environ["SPX_LVL0"] = "batch"
+        ctx = spx.Context(0)
+        ctx.set_comm_shm(a.name, a.rank, a.world)
+        syn, mats, z, nnz = bench.synth_one(spx, 0, a.log_n, a.log_v, 0x5EED0000 + a.log_n)
+        pp = spx.MLProofForR1CS.setup(ctx, a.log_n, 77)
+        pk = spx.IndexPK(ctx, bench.index_from_c(spx, ctx, mats), a.log_n)
+        try:
+            spx.MLArgumentForR1CS.prove(pk, z[: 32 << a.log_v], z[32 << a.log_v :], pp)
+            res = "proved"
+        except spx.InvalidArgument as e:
+            res = "invalid: %s" % e
+        with open(a.out, "w") as f:
+            f.write(res)
+        return
     ctxs = [spx.Context(0) for _ in range(a.inflight)]
     hub = spx.ExchangeHub.shm(a.name, a.rank, a.world) if a.mode == "prove_hub" else None
     for k, c in enumerate(ctxs):

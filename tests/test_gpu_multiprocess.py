@@ -38,3 +38,15 @@ def test_sharded_processes_bit_exact(spx, oc, log_n, mode, inflight):
     want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
     for p in proofs:
         assert p == want
+
+
+@pytest.mark.gpu
+def test_sharded_processes_refuse_mismatched_lvl0_mode(spx):
+    """SPX_LVL0 shapes a proof's exchanges: ranks that read different values must both fail with
+    InvalidArgument on their first sharded proof instead of exchanging mismatched messages"""
+    outs = _run_workers(spx, 2, "lvl0_mismatch", ["--log-n", "8", "--log-v", "3"], timeout=300)
+    res = [open(o).read() for o in outs]
+    for o in outs:
+        os.remove(o)
+    for r in res:
+        assert r.startswith("invalid") and "SPX_LVL0" in r, res

@@ -51,8 +51,8 @@ ISSUE_FILE = os.path.join(ROOT, "profiles", "r02_ubench_issue.txt")
 MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
-KSYM = {"sc1_round": "k_sc1_round<true, false>", "sc2_round": "k_sc2_round<true, false>", "spmv3": "k_sparse3<0>", "mtv3": "k_sparse3<1>",
-        "open_level": "k_open_fold<3>", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
+KSYM = {"sc1_round": "k_sc1_wave<true, false, false>", "sc2_round": "k_sc2_wave<true, false, false>", "spmv3": "k_sparse3<0>",
+        "mtv3": "k_sparse3<1>", "open_level": "k_open_fold_wave<3>", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
         "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq >", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
 KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
           "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]
@@ -341,7 +341,17 @@ def roofline_hbm(stats, pmc_path=PMC_FILE):
             "bytes_per_launch": per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
             "all_launches": {"launches_per_proof": d["launches"], "ms_per_proof": round(d["ms"], 4),
                              "GBs": round(d["bytes"] / (d["ms"] / 1e3) / 1e9, 1)},
+            "largest_launches": {k: largest_rate(stats[k]) for k in cands},
             "note": "algorithmic bytes of the kernel's largest launch / its HIP-event duration, one proof at a time"}
+
+
+def largest_rate(d):
+    """the largest launches of one HBM kernel: algorithmic MB per launch, HIP-event us, GB/s, fraction of HBM peak"""
+    big = d["largest"]
+    us = big["ms"] / big["launches"] * 1e3
+    mb = big["bytes"] / big["launches"] / 1e6
+    gbs = mb / us * 1e3
+    return {"MB": round(mb, 2), "us": round(us, 2), "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 def main():

@@ -30,6 +30,9 @@ struct LongRow {
     uint32_t pad;
     uint64_t x;  // local output index
 };
+// per-block partial sums of one sumcheck round (3 Fr per block, up to 8192 blocks)
+static constexpr uint64_t kRoundPartials = 3 * 8192;
+
 struct Tables3 {
     Fr* t[3];
 };

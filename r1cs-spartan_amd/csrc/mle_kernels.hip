@@ -124,6 +124,13 @@ DEV void block_reduce(Fr (&acc)[K]) {  // result valid in thread 0
 template <int K>
 DEV void grid_reduce_last(Fr (&acc)[K], Fr* __restrict__ partial, uint32_t* __restrict__ ticket, Fr* __restrict__ out) {
     block_reduce<K>(acc);
+    if (gridDim.x == 1) {  // one block: its sum is the result (no hand-off)
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) st_fr(out + k, acc[k]);
+        }
+        return;
+    }
     __shared__ bool last;
     if (threadIdx.x == 0) {
         gu64* dst = (gu64*)(partial + (size_t)blockIdx.x * K);
@@ -385,6 +392,314 @@ __global__ __launch_bounds__(kThreads) void k_sc1_round(Tables3 in, Tables3 out,
         block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
 }
 
+// ------------------------------------------------------------------ small fold rounds, split over lanes
+// The rounds of a few thousand pairs or fewer are latency: a lane's 10 (sumcheck 1) or 6 (sumcheck 2)
+// dependent Fr products at one wave per SIMD. Here one pair is spread over a quad (sumcheck 1: lanes
+// 0, 1, 2 fold A, B, C, lane 3 sums E; then lane 0 adds x0_A x0_B e to G(0), lane 1 adds y_A y_B e to
+// G(2), lane 2 subtracts x0_C e and y_C e: 4 dependent products per lane) or a lane pair (sumcheck 2:
+// lane 0 folds M, lane 1 folds Z; lane 0 adds m0 z0, lane 1 adds (2 m1 - m0)(2 z1 - z0): 3 products),
+// with 4x / 2x the waves. Every lane accumulates its own share; field addition is exact, so the sums
+// equal k_sc1_round's / k_sc2_round's. (For the large rounds this form measured slower than the
+// per-lane one: the wave-transposed kernels below take those.)
+template <int SEL>  // quad_perm: lane i of a quad reads lane SEL[2i+1:2i]
+DEV Fr dpp_fr(const Fr& a) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v[i], SEL, 0xF, 0xF, false);
+    return r;
+}
+DEV Fr sel_fr(bool c, const Fr& a, const Fr& b) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    return r;
+}
+DEV void fold2(Fr& x0, Fr& x1, const Fr* p, const Fr& r) {  // p[0..3] -> (p0 + r(p1-p0), p2 + r(p3-p2))
+    const Fr a0 = ld_fr(p), a1 = ld_fr(p + 1), a2 = ld_fr(p + 2), a3 = ld_fr(p + 3);
+    Fr d;
+    fe_sub(d, a1, a0);
+    fe_mul(d, d, r);
+    fe_add(x0, a0, d);
+    fe_sub(d, a3, a2);
+    fe_mul(d, d, r);
+    fe_add(x1, a2, d);
+}
+template <bool FUSED>
+__global__ __launch_bounds__(kThreads) void k_sc1_fold_quad(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
+                                                            Fr* __restrict__ Eout, const Fr r, uint64_t half,
+                                                            Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                                                            Fr* __restrict__ result3) {
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    const int k = threadIdx.x & 3;
+    const Fr* src = k == 0 ? in.t[0] : k == 1 ? in.t[1] : k == 2 ? in.t[2] : Ein;
+    Fr* dst = k == 0 ? out.t[0] : k == 1 ? out.t[1] : k == 2 ? out.t[2] : Eout;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+    for (uint64_t b = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 2; b < half; b += stride) {
+        Fr x0, x1;
+        if (k < 3) {
+            fold2(x0, x1, src + 4 * b, r);
+            st_fr_fold(dst + 2 * b, x0);
+            st_fr_fold(dst + 2 * b + 1, x1);
+        } else {
+            const Fr e0 = ld_fr(src + 2 * b), e1 = ld_fr(src + 2 * b + 1);
+            fe_add(x0, e0, e1);
+            x1 = x0;
+            if (dst) st_fr_fold(dst + b, x0);
+        }
+        Fr y, P, Q;
+        fe_add(y, x1, x1);
+        fe_sub(y, y, x0);
+        const Fr e = dpp_fr<0xFF>(x0);                       // [3,3,3,3]: lane 3's e
+        const Fr recv = dpp_fr<0xB1>(sel_fr(k == 0, y, x0));  // [1,0,3,2]: lane 0 gets x0_B, lane 1 y_A
+        fe_mul(P, sel_fr(k == 1, y, x0), sel_fr(k == 2, e, recv));
+        fe_mul(Q, sel_fr(k == 2, y, P), e);
+        if (k == 0) {
+            fe_add(g[0], g[0], Q);
+        } else if (k == 1) {
+            fe_add(g[2], g[2], Q);
+        } else if (k == 2) {
+            fe_sub(g[0], g[0], P);
+            fe_sub(g[2], g[2], Q);
+        }
+    }
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+template <bool FUSED>
+__global__ __launch_bounds__(kThreads) void k_sc2_fold_pair(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
+                                                            Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
+                                                            uint64_t half, Fr* __restrict__ partial,
+                                                            uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    const int k = threadIdx.x & 1;
+    const Fr* src = k ? Zin : Min;
+    Fr* dst = k ? Zout : Mout;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) >> 1;
+    for (uint64_t b = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 1; b < half; b += stride) {
+        Fr x0, x1, u, t;
+        fold2(x0, x1, src + 4 * b, r);
+        st_fr_fold(dst + 2 * b, x0);
+        st_fr_fold(dst + 2 * b + 1, x1);
+        fe_add(u, x1, x1);
+        fe_sub(u, u, x0);
+        const Fr recv = dpp_fr<0xB1>(sel_fr(k == 0, u, x0));  // lane 0 gets z0, lane 1 gets 2 m1 - m0
+        fe_mul(t, sel_fr(k == 0, x0, u), recv);
+        if (k == 0)
+            fe_add(g[0], g[0], t);
+        else
+            fe_add(g[2], g[2], t);
+    }
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+
+// ------------------------------------------------------------------ wave-transposed fold rounds
+// The large fold rounds of both sumchecks (round >= 2, P(1) derived on the host). In k_sc1_round a
+// lane reads its own 128-byte runs of every table, so each 16-byte load instruction touches 64
+// different cache lines and reuses each line over 8 instructions; with ~28 KB of lines in flight
+// per wave the L1 cannot hold them, and the lines are fetched again from L2. Here every global load
+// and store instruction is lane-contiguous (one wave covers 1 KB): a wave moves its 64 pairs'
+// inputs through a wave-private LDS region (rows padded to (R + 1) x 16 B, conflict-free) and each
+// lane then reads its own row. Only the wave itself touches its region, so there is no block
+// barrier: LDS operations of one wave complete in order, and `wave_lds_sync` keeps the compiler from
+// moving them across each other.
+#ifndef SPX_SC_WAVE_LDS
+#define SPX_SC_WAVE_LDS 1
+#endif
+#ifndef SPX_SC_WAVES4
+#define SPX_SC_WAVES4 1
+#endif
+#if SPX_SC_WAVES4  // 4 waves per SIMD (a few spilled registers) so a 2^20 round's 4096 waves fit one round
+#define SPX_WAVE_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define SPX_WAVE_OCC
+#endif
+static constexpr int kWaveLdsChunks = 64 * 9;  // 16-byte chunks per wave: 64 rows of up to 8 + 1 pad
+DEV Fr shfl_fr(const Fr& a, int src) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__shfl((int)a.v[i], src, 64);
+    return r;
+}
+DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// a wave's block of 64 * R chunks (global, contiguous) -> lane l's row l (R chunks)
+template <int R>
+DEV void wave_rows_in(const uint4* __restrict__ g, uint4* lds, uint4 (&row)[R], int lane) {
+    uint4 t[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t[k] = g[64 * k + lane];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int c = 64 * k + lane;
+        lds[(c / R) * (R + 1) + c % R] = t[k];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < R; ++j) row[j] = lds[lane * (R + 1) + j];
+    wave_lds_sync();
+}
+// lane l's row l (R chunks) -> the wave's block of 64 * R chunks (global, contiguous)
+template <int R>
+DEV void wave_rows_out(uint4* __restrict__ g, uint4* lds, const uint4 (&row)[R], int lane) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) lds[lane * (R + 1) + j] = row[j];
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int c = 64 * k + lane;
+        g[64 * k + lane] = lds[(c / R) * (R + 1) + c % R];
+    }
+    wave_lds_sync();
+}
+DEV Fr fr_of(const uint4& lo, const uint4& hi) {
+    Fr r;
+    r.v[0] = lo.x, r.v[1] = lo.y, r.v[2] = lo.z, r.v[3] = lo.w;
+    r.v[4] = hi.x, r.v[5] = hi.y, r.v[6] = hi.z, r.v[7] = hi.w;
+    return r;
+}
+DEV void fr_to(uint4& lo, uint4& hi, const Fr& a) {
+    lo = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    hi = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+// one table's 4 inputs of this lane's pair b -> (x0, x1) = (T[4b] + r (T[4b+1] - T[4b]), ...) and
+// the folded pair stored to out[2b], out[2b+1]; `base` = the wave's first pair
+DEV void wave_fold(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t base, const Fr& r, uint4* lds, int lane,
+                   Fr& x0, Fr& x1) {
+    uint4 a[8];
+    wave_rows_in<8>(reinterpret_cast<const uint4*>(in + 4 * base), lds, a, lane);
+    const Fr a0 = fr_of(a[0], a[1]), a1 = fr_of(a[2], a[3]), a2 = fr_of(a[4], a[5]), a3 = fr_of(a[6], a[7]);
+    Fr d;
+    fe_sub(d, a1, a0);
+    fe_mul(d, d, r);
+    fe_add(x0, a0, d);
+    fe_sub(d, a3, a2);
+    fe_mul(d, d, r);
+    fe_add(x1, a2, d);
+    uint4 o[4];
+    fr_to(o[0], o[1], x0);
+    fr_to(o[2], o[3], x1);
+    wave_rows_out<4>(reinterpret_cast<uint4*>(out + 2 * base), lds, o, lane);
+}
+
+// this lane's pair of one table without a fold (round 1): (T[2b], T[2b+1])
+DEV void wave_pair(const Fr* __restrict__ in, uint64_t base, uint4* lds, int lane, Fr& x0, Fr& x1) {
+    uint4 a[4];
+    wave_rows_in<4>(reinterpret_cast<const uint4*>(in + 2 * base), lds, a, lane);
+    x0 = fr_of(a[0], a[1]);
+    x1 = fr_of(a[2], a[3]);
+}
+
+// sumcheck #1 round (FOLD: round >= 2 with the fold of r_{i-1}; NEED1: also G(1)), one wave per 64
+// consecutive pairs (half a multiple of 64); the sums as k_sc1_round
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
+                                                                   Fr* __restrict__ Eout, const Fr r, uint64_t half,
+                                                                   Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                                                                   Fr* __restrict__ result3) {
+    __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
+    uint4* lds = lds_all[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < (half >> 6); w += waves) {
+        const uint64_t base = w << 6;
+        Fr x0[3], x1[3], e;
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            if constexpr (FOLD)
+                wave_fold(in.t[m], out.t[m], base, r, lds, lane, x0[m], x1[m]);
+            else
+                wave_pair(in.t[m], base, lds, lane, x0[m], x1[m]);
+        }
+        if constexpr (FOLD) {
+            uint4 ev[4];
+            wave_rows_in<4>(reinterpret_cast<const uint4*>(Ein + 2 * base), lds, ev, lane);
+            fe_add(e, fr_of(ev[0], ev[1]), fr_of(ev[2], ev[3]));
+            if (Eout) st_fr(Eout + base + lane, e);
+        } else {
+            uint4 ev[2];
+            wave_rows_in<2>(reinterpret_cast<const uint4*>(Ein + base), lds, ev, lane);
+            e = fr_of(ev[0], ev[1]);
+        }
+        Fr t, u, y[3];
+        fe_mul(t, x0[0], x0[1]);
+        fe_sub(t, t, x0[2]);
+        fe_mul(t, t, e);
+        fe_add(g[0], g[0], t);
+        if constexpr (NEED1) {
+            fe_mul(t, x1[0], x1[1]);
+            fe_sub(t, t, x1[2]);
+            fe_mul(t, t, e);
+            fe_add(g[1], g[1], t);
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            fe_add(u, x1[m], x1[m]);
+            fe_sub(y[m], u, x0[m]);
+        }
+        fe_mul(t, y[0], y[1]);
+        fe_sub(t, t, y[2]);
+        fe_mul(t, t, e);
+        fe_add(g[2], g[2], t);
+    }
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+
+// sumcheck #2 round, one wave per 64 consecutive pairs; the sums as k_sc2_round
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
+                                                                   Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
+                                                                   uint64_t half, Fr* __restrict__ partial,
+                                                                   uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+    __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
+    uint4* lds = lds_all[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    Fr g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(g[k]);
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < (half >> 6); w += waves) {
+        const uint64_t base = w << 6;
+        Fr m0, m1, z0, z1, t, u, v;
+        if constexpr (FOLD) {
+            wave_fold(Min, Mout, base, r, lds, lane, m0, m1);
+            wave_fold(Zin, Zout, base, r, lds, lane, z0, z1);
+        } else {
+            wave_pair(Min, base, lds, lane, m0, m1);
+            wave_pair(Zin, base, lds, lane, z0, z1);
+        }
+        fe_mul(t, m0, z0);
+        fe_add(g[0], g[0], t);
+        if constexpr (NEED1) {
+            fe_mul(t, m1, z1);
+            fe_add(g[1], g[1], t);
+        }
+        fe_add(u, m1, m1);
+        fe_sub(u, u, m0);
+        fe_add(v, z1, z1);
+        fe_sub(v, v, z0);
+        fe_mul(t, u, v);
+        fe_add(g[2], g[2], t);
+    }
+    if constexpr (FUSED)
+        grid_reduce_last<3>(g, partial, ticket, result3);
+    else
+        block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+
 // ------------------------------------------------------------------ sumcheck #2 round
 // tables M (= sum_m r_m M(r_x, .)) and Z; partial = (P(0), P(1), P(2)), P(t) = sum_b M_t Z_t
 // (need1 == 0: P(1) left 0, derived on the host).
@@ -495,6 +810,86 @@ __global__ __launch_bounds__(kThreads) void k_open_fold(const Fr* __restrict__ r
     }
 }
 
+// k_open_fold with every global access lane-contiguous (the wave-transposed form of the sumcheck
+// rounds above). A lane folds one group of 4 consecutive entries through two levels (2 + 1
+// quotients, one output u): NF = 2 takes the wave's 64 outputs directly; NF = 3 takes the 128 groups
+// behind its 64 outputs in two halves, and the third level combines the u of lanes 2k, 2k+1 (DPP).
+DEV void fold_group4(const uint4 (&a)[8], const FoldArgs<3>& fa, int j0, Fr (&q0)[2], Fr& q1, Fr& u) {
+    Fr v[4], t;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = fr_of(a[2 * k], a[2 * k + 1]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        fe_sub(q0[k], v[2 * k + 1], v[2 * k]);
+        fe_mul(t, q0[k], fa.p[j0]);
+        fe_add(v[k], v[2 * k], t);
+    }
+    fe_sub(q1, v[1], v[0]);
+    fe_mul(t, q1, fa.p[j0 + 1]);
+    fe_add(u, v[0], t);
+}
+DEV void wave_store_q(Fr* __restrict__ q, uint64_t qoff, uint64_t first, const Fr (&q0)[2], uint4* lds, int lane) {
+    uint4 o[4];
+    fr_to(o[0], o[1], q0[0]);
+    fr_to(o[2], o[3], q0[1]);
+    wave_rows_out<4>(reinterpret_cast<uint4*>(q + qoff + 2 * first), lds, o, lane);
+}
+DEV void wave_store_1(Fr* __restrict__ dst, const Fr& x, uint4* lds, int lane) {
+    uint4 o[2];
+    fr_to(o[0], o[1], x);
+    wave_rows_out<2>(reinterpret_cast<uint4*>(dst), lds, o, lane);
+}
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold_wave(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+                                                             Fr* __restrict__ q, FoldArgs<NF> a, uint64_t nout) {
+    static_assert(NF == 2 || NF == 3, "2 or 3 levels");
+    __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
+    uint4* lds = lds_all[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    FoldArgs<3> fa;  // levels j0, j0 + 1 of fold_group4
+#pragma unroll
+    for (int j = 0; j < NF; ++j) fa.p[j] = a.p[j];
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < (nout >> 6); w += waves) {
+        const uint64_t base = w << 6;  // first output of this wave
+        if constexpr (NF == 2) {
+            uint4 in[8];
+            wave_rows_in<8>(reinterpret_cast<const uint4*>(rin + 4 * base), lds, in, lane);
+            Fr q0[2], q1, u;
+            fold_group4(in, fa, 0, q0, q1, u);
+            if (a.qoff[0] != ~0ull) wave_store_q(q, a.qoff[0], base, q0, lds, lane);
+            if (a.qoff[1] != ~0ull) wave_store_1(q + a.qoff[1] + base, q1, lds, lane);
+            wave_store_1(rout + base, u, lds, lane);
+        } else {
+            Fr q2 = {}, r = {};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint64_t grp = 2 * base + 64 * h;  // first group of this half (group = 4 entries)
+                uint4 in[8];
+                wave_rows_in<8>(reinterpret_cast<const uint4*>(rin + 4 * grp), lds, in, lane);
+                Fr q0[2], q1, u, t;
+                fold_group4(in, fa, 0, q0, q1, u);
+                if (a.qoff[0] != ~0ull) wave_store_q(q, a.qoff[0], grp, q0, lds, lane);
+                if (a.qoff[1] != ~0ull) wave_store_1(q + a.qoff[1] + grp, q1, lds, lane);
+                const Fr un = dpp_fr<0xB1>(u);  // [1,0,3,2]: the pair partner's u
+                Fr d;
+                fe_sub(d, un, u);  // even lane: u_odd - u_even = level 2's quotient
+                fe_mul(t, d, a.p[2]);
+                fe_add(t, u, t);
+                // gather the even lanes' results of this half into lanes 32 h .. 32 h + 31
+                const int src = 2 * (lane & 31);
+                const Fr dq = shfl_fr(d, src), dr = shfl_fr(t, src);
+                if ((lane >> 5) == h) {
+                    q2 = dq;
+                    r = dr;
+                }
+            }
+            if (a.qoff[2] != ~0ull) st_fr(q + a.qoff[2] + base + lane, q2);
+            st_fr(rout + base + lane, r);
+        }
+    }
+}
+
 // The last levels of an opening in ONE launch (one block, the table in LDS): level j folds
 // half = h0 >> j pairs, q_j = the level's quotients (q + qoff_j, contiguous), r' as k_open_level.
 // The final one-entry table goes to `last`. (Launched per level these small folds were latency: one
@@ -587,6 +982,10 @@ int sc_grid(uint64_t half) { return grid_for(half, 1024); }
 // Rounds whose grid has few blocks reduce in their last block (one launch); large grids keep a
 // separate one-block reduction launch, so the streaming kernel's own duration carries no serial tail.
 static constexpr int kFuseMaxBlocks = 64;
+// wave-transposed fold rounds (k_sc1_fold_wave, k_sc2_fold_wave) for the large rounds only (whole
+// waves of 64 pairs; grids of <= kFuseMaxBlocks blocks reduce in their last block, as k_sc1_round)
+static constexpr uint64_t kWaveMinHalf = 1u << 14;
+static constexpr int kWaveMaxBlocks = (int)(kRoundPartials / 3);
 template <bool FOLD>
 static void sc1_launch(int g, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r, uint64_t half,
                        Fr* partial, uint32_t* ticket, Fr* result3, int need1, hipStream_t s) {
@@ -608,11 +1007,46 @@ static void sc2_launch(int g, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, 
                            partial, ticket, result3, need1);
 }
 
+template <bool FOLD, bool NEED1>
+static void sc1_wave_launch(int g, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
+                            uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc1_wave<FOLD, NEED1, true>), dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half,
+                           partial, ticket, result3);
+    else
+        hipLaunchKernelGGL((k_sc1_wave<FOLD, NEED1, false>), dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half,
+                           partial, ticket, result3);
+}
+template <bool FOLD, bool NEED1>
+static void sc2_wave_launch(int g, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
+                            Fr* partial, uint32_t* ticket, Fr* result3, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc2_wave<FOLD, NEED1, true>), dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half,
+                           partial, ticket, result3);
+    else
+        hipLaunchKernelGGL((k_sc2_wave<FOLD, NEED1, false>), dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r,
+                           half, partial, ticket, result3);
+}
+
 void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr* Ein, Fr* Eout, const Fr& r,
                       uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC1, s);
-    if (fold)
+    if (SPX_SC_WAVE_LDS && half >= kWaveMinHalf) {
+        g = grid_for(half, kWaveMaxBlocks);
+        if (fold && need1)
+            sc1_wave_launch<true, true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
+        else if (fold)
+            sc1_wave_launch<true, false>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
+        else if (need1)
+            sc1_wave_launch<false, true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
+        else
+            sc1_wave_launch<false, false>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
+    } else if (SPX_SC_WAVE_LDS && fold && !need1) {  // small fold round: quad per pair, last-block reduction
+        g = grid_for(4 * half, kFuseMaxBlocks);
+        hipLaunchKernelGGL(k_sc1_fold_quad<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial,
+                           ticket, result3);
+    } else if (fold)
         sc1_launch<true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     else
         sc1_launch<false>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
@@ -625,7 +1059,21 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
                       Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC2, s);
-    if (fold)
+    if (SPX_SC_WAVE_LDS && half >= kWaveMinHalf) {
+        g = grid_for(half, kWaveMaxBlocks);
+        if (fold && need1)
+            sc2_wave_launch<true, true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
+        else if (fold)
+            sc2_wave_launch<true, false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
+        else if (need1)
+            sc2_wave_launch<false, true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
+        else
+            sc2_wave_launch<false, false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
+    } else if (SPX_SC_WAVE_LDS && fold && !need1) {  // small fold round: lane pair per pair
+        g = grid_for(2 * half, kFuseMaxBlocks);
+        hipLaunchKernelGGL(k_sc2_fold_pair<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
+                           ticket, result3);
+    } else if (fold)
         sc2_launch<true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     else
         sc2_launch<false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
@@ -655,14 +1103,21 @@ void launch_open_fold(const Fr* rin, Fr* rout, Fr* q, int nf, const Fr* points, 
     const int g = grid_for(nout, 8192);
     double qw = 0;
     for (int j = 0; j < nf; ++j) qw += qoffs[j] != ~0ull ? (double)(nout << (nf - 1 - j)) : 0.0;
+    const bool wave = SPX_SC_WAVE_LDS && nout >= kWaveMinHalf;  // whole waves of 64 outputs
     if (nf == 3) {
         FoldArgs<3> a;
         for (int j = 0; j < 3; ++j) a.p[j] = points[j], a.qoff[j] = qoffs[j];
-        hipLaunchKernelGGL(k_open_fold<3>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+        if (wave)
+            hipLaunchKernelGGL(k_open_fold_wave<3>, dim3(grid_for(nout, 8192)), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+        else
+            hipLaunchKernelGGL(k_open_fold<3>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
     } else if (nf == 2) {
         FoldArgs<2> a;
         for (int j = 0; j < 2; ++j) a.p[j] = points[j], a.qoff[j] = qoffs[j];
-        hipLaunchKernelGGL(k_open_fold<2>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+        if (wave)
+            hipLaunchKernelGGL(k_open_fold_wave<2>, dim3(grid_for(nout, 8192)), dim3(kThreads), 0, s, rin, rout, q, a, nout);
+        else
+            hipLaunchKernelGGL(k_open_fold<2>, dim3(g), dim3(kThreads), 0, s, rin, rout, q, a, nout);
     } else {
         throw std::invalid_argument("launch_open_fold: 2 or 3 levels");
     }

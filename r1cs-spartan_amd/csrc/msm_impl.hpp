@@ -532,26 +532,36 @@ __global__ __launch_bounds__(kTopThreads, 1) void k_tree_top(const MsmInst* __re
         cur ^= 1;
         nin = nout;
     }
-    if (I.lg && grp == 0) {  // the rank's share of a split instance: G F - (G - 1 - sel) S
-        X29<T> f, sv, acc;
-        A::ld(f, &buf[cur][0][0]);
-#pragma unroll 1
-        for (uint32_t d = 0; d < I.lg; ++d) tree_dbl<F>(f);
+    if (I.lg) {  // the rank's share of a split instance: G F - (G - 1 - sel) S, the two products side by side
         const uint32_t k = (1u << I.lg) - 1 - I.sel;
-        if (k) {
+        if (grp == 0) {  // G F: lg doublings
+            X29<T> f;
+            A::ld(f, &buf[cur][0][0]);
+#pragma unroll 1
+            for (uint32_t d = 0; d < I.lg; ++d) tree_dbl<F>(f);
+            A::st(&buf[cur][0][0], f);
+        } else if (grp == 1 && k) {  // -(k S): double-and-add below the top bit, into the free slot
+            X29<T> sv, acc;
             A::ld(sv, &buf[cur][1][0]);
             acc = sv;
 #pragma unroll 1
-            for (int b = 30 - __clz(k); b >= 0; --b) {  // k S, double-and-add below the top bit
+            for (int b = 30 - __clz(k); b >= 0; --b) {
                 tree_dbl<F>(acc);
                 if ((k >> b) & 1u) tree_add<F>(acc, sv);
             }
             T z;
             O::zero(z);
-            O::template sub<2>(acc.y, z, acc.y);  // -(k S): y < 2p -> 2p - y < 2p
-            tree_add<F>(f, acc);
+            O::template sub<2>(acc.y, z, acc.y);  // y < 2p -> 2p - y < 2p
+            A::st(&buf[cur][1][1], acc);
         }
-        A::st(&buf[cur][0][0], f);
+        __syncthreads();
+        if (grp == 0 && k) {
+            X29<T> f, acc;
+            A::ld(f, &buf[cur][0][0]);
+            A::ld(acc, &buf[cur][1][1]);
+            tree_add<F>(f, acc);
+            A::st(&buf[cur][0][0], f);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // back to the R = 2^384 Montgomery domain, canonical, for the host

@@ -967,7 +967,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
                           + n                // eq(r_x)
                           + nl + n2 + n4     // Mrx + fold
                           + n2 + n4          // z fold
-                          + std::max<uint64_t>(3 * 2048, std::max(I.rows.nchunks, I.cols.nchunks))
+                          + std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.nchunks))
                           + 8192 * 2 + 64 + 8 * L;  // partials, eq scratch, challenges
     C.scratch.ensure(32 * need);
     Fr* base = C.scratch.as<Fr>();
@@ -984,7 +984,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Fr* EQ = take(n);
     Fr *M0 = take(nl), *M1 = take(n2), *M2 = take(n4);
     Fr *Z1 = take(n2), *Z2 = take(n4);
-    Fr* partial = take(std::max<uint64_t>(3 * 2048, std::max(I.rows.nchunks, I.cols.nchunks)));
+    Fr* partial = take(std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.nchunks)));
     Fr *eqlo = take(8192), *eqhi = take(8192);
     Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
     uint8_t* hp = C.pin_at(Ctx::kPinHp, 1 << 16, 64 << 10);

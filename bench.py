@@ -13,7 +13,7 @@ witnesses (default: one per proof of a step), so every proof has its own transcr
 scalars and gather streams.
 
 One step = P = --proofs-per-step proofs (default 64) over the W witnesses; the K timed steps run
-as one continuous pipeline of K x P proofs through spx_prove_many with B = --inflight (default 16)
+as one continuous pipeline of K x P proofs through spx_prove_many with B = --inflight (default: inflight_for)
 host worker threads, each with its own HIP stream and MSM workspace, so the sequential host Blake2s
 absorption of the matrices (~150 MB per proof, one pool of hashing threads per rank) overlaps other
 proofs' GPU work. value = constraints proved per second over the timed region (whole job).
@@ -36,6 +36,7 @@ import ctypes
 import importlib.util
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -129,7 +130,6 @@ def oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
     so = os.path.join(ROOT, "oracle", "liboracle.so")
     if not os.path.exists(so):
-        import subprocess
 
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     import oracle_c as oc
@@ -354,6 +354,26 @@ def largest_rate(d):
     return {"MB": round(mb, 2), "us": round(us, 2), "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def inflight_for(g):
+    """proofs in flight per rank for proofs sharded over g ranks (1: unsharded). Solo-rank sweeps on one
+    MI355X (profiles/r03/r03ak_inflight_hwq.jsonl, 32 hardware queues): 16 is best at g <= 2; a rank of
+    a 4- or 8-rank proof has 1/g of every kernel's work, so it needs 8 g proofs in flight to fill the GPU"""
+    return 16 if g <= 2 else min(64, 8 * g)
+
+
+def hw_queues_for(g):
+    """hardware queues per process (GPU_MAX_HW_QUEUES): 16 for up to 16 proofs in flight (32 measured
+    1% slower at N = 1, profiles/r03/r03al_ab_hwq.jsonl); 32 when 4- or 8-rank proofs keep 32-64 in flight
+    (profiles/r03/r03aj_g8_knobs.jsonl: 64 in flight on 32 queues +18% over 16 on 16)"""
+    return 16 if g <= 2 else 32
+
+
+def lvl0_for(g):
+    """level-0 opening MSM inside the first opening's batch (one MSM pipeline less per proof) for proofs
+    sharded over g >= 4 ranks, where a rank's small MSMs are latency-bound; beside the commitment otherwise"""
+    return 1 if g >= 4 else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -387,7 +407,9 @@ def main():
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
                     help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (one communicator per rank "
                     "shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm)")
-    ap.add_argument("--inflight", type=int, default=16, help="proofs in flight (worker contexts)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="proofs in flight per rank (worker contexts); default: 16 for unsharded and 2-rank proofs, "
+                    "8 x G (at most 64) for proofs sharded over G >= 4 ranks (inflight_for)")
     ap.add_argument("--proofs-per-step", type=int, default=64,
                     help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
     args = ap.parse_args()
@@ -416,13 +438,15 @@ def main():
     # host waits sleep rather than spin: with many proofs in flight the cores go to the transcript
     # hashing pool of spx_prove_many (measured: 31.2 vs 28.2 M constraints/s at 2^20 on one MI355X)
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
-    # 16 hardware queues per process (HIP default 4): a proof's small latency-bound kernels (sumcheck
+    # hardware queues per process (HIP default 4): a proof's small latency-bound kernels (sumcheck
     # rounds, bucket-weighting levels) then queue behind fewer of the other proofs' MSM launches
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
     spx = load_product()
     L = spx.lib()
-    B = max(1, args.inflight)
-    P = max(B, (args.proofs_per_step + B - 1) // B * B)  # proofs per step; each worker proves P / B of them
+    Bb = args.inflight or inflight_for(1)  # contexts of the unsharded (batch) proofs
+    Bs = args.inflight or inflight_for(world)  # contexts of the proofs sharded over all ranks
+    Bm = max(Bb, Bs, inflight_for(2))
+    P = max(Bm, (args.proofs_per_step + Bm - 1) // Bm * Bm)  # proofs per step; each worker proves P / B of them
     # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
     device = 0 if os.environ.get("SPX_BENCH_SAME_GPU") == "1" else local
     sharded_head = world > 1 and args.shard == "proof"
@@ -431,6 +455,8 @@ def main():
 
     def make_sharded(k):
         cs = [spx.Context(device) for _ in range(k)]
+        for c in cs:
+            c.set_lvl0_batch(lvl0_for(world))
         if args.comm == "rccl":
             # ONE communicator per rank; every proof in flight exchanges through its own channel of
             # the ordered hub (comm_hub.cpp), context j on channel j on every rank
@@ -447,8 +473,8 @@ def main():
                 c.set_comm_shm("%s_%d" % (name[0], j), rank, world)
         return cs
 
-    ctxs = [spx.Context(device) for _ in range(B)] if need_batch else []
-    sctxs = make_sharded(B) if need_sharded else []
+    ctxs = [spx.Context(device) for _ in range(Bb)] if need_batch else []
+    sctxs = make_sharded(Bs) if need_sharded else []
     ctx = (ctxs or sctxs)[0]
 
     n = 1 << log_n
@@ -507,7 +533,7 @@ def main():
     proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps))
     stats = {}
     if not args.no_stats:
-        stats = kernel_stats(spx, L, hctx, args.steps * (P // B))  # ctx 0 proves P / B proofs per step
+        stats = kernel_stats(spx, L, hctx, args.steps * (P // len(hctxs)))  # ctx 0 proves P / B proofs per step
         spx._check(L.spx_kernel_stats_enable(hctx.h, 0))
     ref = check_batch(proofs)
     # ---- single-proof latency (one proof at a time), with and without the index-cached transcript.
@@ -552,8 +578,9 @@ def main():
                 continue
             gname = [spx.shm_name() if rank == 0 else None]
             dist.broadcast_object_list(gname, src=0)
-            gctxs = [spx.Context(device) for _ in range(B)]
+            gctxs = [spx.Context(device) for _ in range(args.inflight or inflight_for(K))]
             for j, c in enumerate(gctxs):
+                c.set_lvl0_batch(lvl0_for(K))
                 c.set_comm_shm("%s_g%d_%d" % (gname[0], rank // K, j), rank % K, K)
             gpk = spx.IndexPK(gctxs[0], index_from_c(spx, gctxs[0], mats), log_n)
             batch_fn(gctxs, gpk, 1)()
@@ -567,23 +594,28 @@ def main():
     # the rank does a real rank's device and host work for its 1/G of the buckets, blocks and hashing.
     # Every rank of the node does the same on its own GPU, so the node's rate is this rank's proof rate
     # (exchange latency taken as free; the proofs of a rehearsal are not valid and are not checked).
+    # Each G runs in a child process of its own (tools/vrank_bench.py --solo), with the settings an N = G
+    # rank runs with: inflight_for(G) proofs in flight, lvl0_for(G), hw_queues_for(G) hardware queues
+    # (a process-wide HIP setting), and none of this process's contexts sharing its queues.
     rehearsal = None
     if world == 1 and args.rehearse and not stub:
-        rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free); "
-                     "node value = the rank's proof rate x n", "proofs_in_flight": B, "values": {}, "msm_reruns": {}}
+        rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free), "
+                     "matrices absorbed per proof (1/G of them by this rank), in a child process "
+                     "(tools/vrank_bench.py --solo); node value = the rank's proof rate x n",
+                     "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "msm_reruns": {}}
         for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
-            rc = [spx.Context(device) for _ in range(B)]
-            for c in rc:
-                c.set_comm_rehearsal(0, G)
-            rk = spx.IndexPK(rc[0], index_from_c(spx, rc[0], mats), log_n)
-            wl = [wits[i % W] for i in range(P)]
-            spx.MLArgumentForR1CS.prove_many(rc, rk, wl, pp, mode=args.mode, seed=7)
-            t0 = time.perf_counter()
-            spx.MLArgumentForR1CS.prove_many(rc, rk, wl * args.steps, pp, mode=args.mode, seed=7)
-            el = time.perf_counter() - t0
-            rehearsal["values"][str(G)] = round(P * args.steps * n / el, 1)
-            rehearsal["msm_reruns"][str(G)] = sum(c.msm_reruns() for c in rc)
-            del rk, rc
+            env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues_for(G)))
+            cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo",
+                   "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P), "--steps", str(args.steps),
+                   "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
+            r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+            if r.returncode != 0:
+                raise RuntimeError("rehearsal G=%d failed: %s" % (G, r.stderr[-2000:]))
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            rehearsal["values"][str(G)] = d["node_estimate"]
+            rehearsal["proofs_in_flight"][str(G)] = d["inflight_per_rank"]
+            rehearsal["hw_queues"][str(G)] = hw_queues_for(G)
+            rehearsal["msm_reruns"][str(G)] = d["msm_reruns"]
 
     ms = elapsed / args.steps * 1e3  # per step (P proofs)
     ms_c = elapsed_cached / args.steps * 1e3 if elapsed_cached else 0.0
@@ -653,7 +685,7 @@ def main():
     wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
         KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
         "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
-        args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, B)
+        args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, len(hctxs))
     out = {
         "metric": "R1CS constraints proved/sec at 2^%d%s" % (log_n, " (sumcheck-only, commitment stubbed)" if stub else ""),
         "value": round(jobs * n / (ms / 1e3), 1),
@@ -674,7 +706,7 @@ def main():
             "baseline_config": "C2" if stub else "C3",
             "distinct_witnesses": W,
             "proofs_per_step": P,
-            "proofs_in_flight": B,
+            "proofs_in_flight": len(hctxs),
             "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
             "comm": args.comm if sctxs else None,
         },
@@ -719,7 +751,7 @@ def main():
         rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
         out["proof_sharded_rehearsal"] = rehearsal
     if not stub and world == 1 and not args.no_c2:
-        out["c2"] = c2_line(spx, L, args, B)
+        out["c2"] = c2_line(spx, L, args, Bb)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -114,6 +114,12 @@ int spx_ctx_set_comm_group(spx_ctx *ctx, void *group, int rank);
  * (every exchange returns its own contribution in all slots): the device and host work of one rank
  * on a GPU of its own, for throughput estimates of an N-GPU node. Its proofs are not valid. */
 int spx_ctx_set_comm_rehearsal(spx_ctx *ctx, int rank, int world);
+/* Where the shared level-0 opening MSM of a proof runs (no effect on the proof bytes): 0 = beside the
+ * commitment (its own MSM pipeline, the default), 1 = inside the first opening's MSM batch (one MSM
+ * pipeline less per proof: sort, weighting tree), -1 = the process default (SPX_LVL0=batch -> 1).
+ * Every rank of a proof-sharded prove must use the same mode (checked on the context's first sharded
+ * proof: SPX_INVALID_ARGUMENT otherwise). */
+int spx_ctx_set_lvl0_batch(spx_ctx *ctx, int mode);
 /* one allgather on the context's communicator (whatever its transport): every rank passes `bytes`,
  * recv receives world * bytes in rank order. For transport tests. */
 int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t bytes);

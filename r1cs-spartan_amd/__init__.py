@@ -83,6 +83,7 @@ EXPORTED = [
     "spx_comm_group_destroy",
     "spx_ctx_set_comm_group",
     "spx_ctx_set_comm_rehearsal",
+    "spx_ctx_set_lvl0_batch",
     "spx_comm_hub_create_rccl",
     "spx_comm_hub_create_shm",
     "spx_comm_hub_create_group",
@@ -152,6 +153,8 @@ def lib():
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
     L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
+        L.spx_ctx_set_lvl0_batch.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_comm_hub_create_rccl") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate the hub
         L.spx_comm_hub_create_rccl.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.spx_comm_hub_create_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
@@ -292,6 +295,11 @@ class Context:
         """one rank of a world-rank proof-sharded prove without its peers (throughput rehearsal; the
         proofs are not valid)"""
         _check(lib().spx_ctx_set_comm_rehearsal(self.h, int(rank), int(world)))
+
+    def set_lvl0_batch(self, mode):
+        """where the shared level-0 opening MSM runs: 1 inside the first opening's batch, 0 beside the
+        commitment, -1 the process default (SPX_LVL0); the same on every rank of a sharded prove"""
+        _check(lib().spx_ctx_set_lvl0_batch(self.h, int(mode)))
 
     def comm_allgather(self, data, world):
         """one allgather of `data` on this context's communicator -> list of world byte strings"""

@@ -217,6 +217,15 @@ int spx_ctx_set_comm_rehearsal(spx_ctx* ctx, int rank, int world) {
     });
 }
 
+int spx_ctx_set_lvl0_batch(spx_ctx* ctx, int mode) {
+    return guard([&] {
+        if (!ctx) spx::invalid("null context");
+        if (mode < -1 || mode > 1) spx::invalid("level-0 mode must be -1, 0 or 1");
+        ctx->c->lvl0_mode = mode;
+        ctx->c->knobs_agreed = false;
+    });
+}
+
 int spx_ctx_comm_allgather(spx_ctx* ctx, const void* send, void* recv, size_t bytes) {
     return guard([&] {
         set_dev(ctx);

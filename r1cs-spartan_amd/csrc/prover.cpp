@@ -1004,10 +1004,11 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     // batches, so the exchanges of a proof-sharded prove line up.)
     // SPX_LVL0=batch (A/B; must be the same on every rank of a proof-sharded prove): level 0 inside the
     // first opening's MSM batch instead, one MSM pipeline (sort, weighting tree) less per proof
-    static const bool lvl0_batch = [] {
+    static const bool lvl0_batch_env = [] {
         const char* e = getenv("SPX_LVL0");
         return e && std::string(e) == "batch";
     }();
+    const bool lvl0_batch = C.lvl0_mode >= 0 ? C.lvl0_mode == 1 : lvl0_batch_env;
     if (G > 1 && !C.knobs_agreed) {
         // the level-0 mode decides the order and sizes of a proof's exchanges: every rank of the
         // communicator must read the same SPX_LVL0 (one exchange on a context's first sharded proof)
@@ -1015,7 +1016,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         std::vector<uint32_t> all(G);
         comm.allgather(&mine, all.data(), sizeof mine);
         for (int r = 0; r < G; ++r)
-            if (all[r] != mine) invalid("SPX_LVL0 differs between the ranks of this communicator");
+            if (all[r] != mine) invalid("SPX_LVL0 / level-0 mode differs between the ranks of this communicator");
         C.knobs_agreed = true;
     }
     const bool share0 = !o.stub;

@@ -184,7 +184,9 @@ struct Ctx {
     std::vector<std::pair<std::string, double>> timings;
     KProf kprof;
     uint64_t prove_seq = 0;  // proofs started on this context (identical on every rank of its communicator)
-    bool knobs_agreed = false;  // exchange-shaping env knobs checked equal across the communicator
+    bool knobs_agreed = false;  // exchange-shaping knobs checked equal across the communicator
+    int lvl0_mode = -1;         // shared level-0 opening MSM: 1 inside the first opening's batch, 0 beside
+                                // the commitment, -1 the process default (SPX_LVL0=batch -> 1)
     std::atomic<uint64_t> msm_reruns{0};  // MSM batches rerun dense after a compacted-key overflow
     Ctx(int dev);
     ~Ctx();

@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
+def _prove_ranks(spx, G, inst, ppb, w_bytes=None, lvl0=None):
     group = spx.CommGroup(G)
     out = [None] * G
     reruns = [0] * G
@@ -22,6 +22,8 @@ def _prove_ranks(spx, G, inst, ppb, w_bytes=None):
         try:
             ctx = spx.Context(0)
             ctx.set_comm_group(group, r)
+            if lvl0 is not None:
+                ctx.set_lvl0_batch(lvl0[r])
             pp = spx.PublicParameter.load(ctx, ppb)
             mats = [spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats]
             pk = spx.MLArgumentForR1CS.index(ctx, *mats)
@@ -108,3 +110,24 @@ def test_rehearsal_rank_runs(spx, oc):
         assert len(got) == len(want)
         assert (got == want) == (G == 1)
         assert ctx.msm_reruns() == 0
+
+
+def test_virtual_ranks_level0_in_first_batch(spx, oc):
+    """spx_ctx_set_lvl0_batch(1) on every rank: the shared level-0 opening MSM inside the first
+    opening's batch (bench.py's setting at G >= 4) gives the same bytes"""
+    log_n, log_v, G = 10, 3, 4
+    inst = oc.Instance(0, log_n, log_v, 980 + log_n, 0)
+    ppb = oc.PP.keygen(log_n, 981).serialize()
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, oc.PP.load(ppb), 0, 0)
+    out, reruns = _prove_ranks(spx, G, inst, ppb, lvl0=[1] * G)
+    assert all(p == want for p in out)
+
+
+def test_virtual_ranks_level0_mode_mismatch(spx, oc):
+    """ranks that disagree on the level-0 mode fail on their first sharded proof (no mismatched exchanges)"""
+    log_n, log_v, G = 8, 3, 2
+    inst = oc.Instance(0, log_n, log_v, 990 + log_n, 0)
+    ppb = oc.PP.keygen(log_n, 991).serialize()
+    with pytest.raises(AssertionError) as e:
+        _prove_ranks(spx, G, inst, ppb, lvl0=[1, 0])
+    assert "level-0 mode differs" in str(e.value)

@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--G", type=int, default=4)
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--log-v", type=int, default=5)
-    ap.add_argument("--inflight", type=int, default=4, help="contexts (proofs in flight) per rank")
+    ap.add_argument("--inflight", type=int, default=0, help="contexts (proofs in flight) per rank (default: bench.inflight_for)")
+    ap.add_argument("--lvl0", type=int, default=-2, help="level-0 opening MSM mode per context (default: bench.lvl0_for)")
     ap.add_argument("--proofs", type=int, default=64, help="proofs per step")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
@@ -34,7 +35,7 @@ def main():
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     spx = bench.load_product()
-    G, B, P = a.G, a.inflight, a.proofs
+    G, B, P = a.G, a.inflight or bench.inflight_for(a.G), a.proofs
     world = G
     if a.solo:
         G = 1  # one rank object, acting as rank 0 of `world`
@@ -42,6 +43,7 @@ def main():
     ctxs = [[spx.Context(0) for _ in range(B)] for _ in range(G)]
     for r in range(G):
         for k in range(B):
+            ctxs[r][k].set_lvl0_batch(bench.lvl0_for(world) if a.lvl0 == -2 else a.lvl0)
             if a.solo:
                 ctxs[r][k].set_comm_rehearsal(0, world)
             elif G > 1:

@@ -371,7 +371,15 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             cv.notify_all();
         }
     };
-    int nh = nctx;
+    // Pool size: the hashers run ahead as fast as they can, so a pool larger than the cores it needs
+    // starves the proof threads of their host work (solo G = 8 rank, 64 in flight on 16 cores: 64
+    // hashers 332 M, 8 hashers 381 M constraints/s; profiles/r03/r03am_hash_threads.jsonl). A rank of a
+    // G-rank proof absorbs 1/G of the proofs: half the core budget for G >= 4, all of it otherwise.
+    // Budget: SPX_HASH_THREADS, else OMP_NUM_THREADS (the box's CPU share), else the hardware threads.
+    int budget = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("OMP_NUM_THREADS")) budget = atoi(e);
+    budget = std::max(1, budget);
+    int nh = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
     if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
     nh = std::min<int>(nh, (int)owned.size());
     std::vector<std::thread> pool;

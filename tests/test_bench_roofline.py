@@ -51,3 +51,24 @@ def test_whole_proof_valu_excludes_setup_kernels(bench):
     acc = sum(ks[k]["SQ_INSTS_VALU_per_launch"] * ks[k]["launches_valu_pass"] for k in ("k_accum_aff<Fq2>", "k_accum_aff<Fq >"))
     assert acc / proofs < wp["valu_insts_per_proof"] < 1.3 * acc / proofs
     assert 0 < wp["frac"] < 1
+
+
+def test_settings_by_sharding_degree(bench):
+    """proofs in flight / hardware queues / level-0 mode per sharding degree: the
+    measured optima, every in-flight count divides the default 64 proofs per step, and the RCCL hub's
+    64 channels cover the largest"""
+    assert [bench.inflight_for(g) for g in (1, 2, 4, 8, 16)] == [16, 16, 32, 64, 64]
+    assert [bench.hw_queues_for(g) for g in (1, 2, 4, 8)] == [16, 16, 32, 32]
+    assert [bench.lvl0_for(g) for g in (1, 2, 4, 8)] == [0, 0, 1, 1]
+    for g in (1, 2, 4, 8):
+        assert 64 % bench.inflight_for(g) == 0
+        assert bench.hw_queues_for(g) <= 32  # gpurun / the pool refuse more
+
+
+def test_hbm_largest_launch_rates(bench):
+    """every HBM kernel's largest launch: algorithmic MB over its HIP-event duration"""
+    r = bench.largest_rate({"largest": {"launches": 2, "ms": 0.1, "bytes": 2 * 176e6}})
+    assert r["MB"] == pytest.approx(176.0)
+    assert r["us"] == pytest.approx(50.0)
+    assert r["GBs"] == pytest.approx(3520.0)
+    assert r["frac"] == pytest.approx(0.44)

@@ -23,6 +23,8 @@
 // Many MSMs run as one batch (all nv levels of an opening), and nothing in it waits for the host.
 #include "msm_common.hpp"
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -385,6 +387,20 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
     p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
 }
 
+#ifndef SPX_SORT_BITS
+#define SPX_SORT_BITS 0  // A/B knob: 11-bit rocPRIM onesweep digits measured no faster (profiles/r03/r03at_ab_sort_bits.jsonl)
+#endif
+#ifndef SPX_SORT_MERGE_LIMIT  // below this many keys rocPRIM sorts by merging (its default: 2^20)
+#define SPX_SORT_MERGE_LIMIT (1024 * 1024)
+#endif
+#if SPX_SORT_BITS
+using SortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, SPX_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    SPX_SORT_MERGE_LIMIT>;
+#endif
+
 MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s) {
     MsmSorted o;
     const uint32_t nb = p.nb;
@@ -425,13 +441,27 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
         hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, ka, va, n, nb,
                            o.offs, hist, o.refs);
     } else {
+#if SPX_SORT_BITS
+        // rocPRIM onesweep with SPX_SORT_BITS-bit digits (the gfx950 default is 8): the bucket keys of an
+        // opening batch span 17-20 bits (2^15 / G buckets x ~20 instances), so 2 passes instead of 3.
+        // Measured: the sort's time per proof is unchanged at N = 1 and G = 8 is 2% slower, so it is off.
+        rocprim::double_buffer<uint32_t> dk(ka, kb), dv(va, o.refs);
+        size_t tb = 0;
+        HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, dk, dv, n, 0u, (unsigned)bits, s));
+        void* t = ws->cub.ensure(tb);
+        HIPCHK(rocprim::radix_sort_pairs<SortCfg>(t, tb, dk, dv, n, 0u, (unsigned)bits, s));
+        o.refs = dv.current();
+        const uint32_t* sorted = dk.current();
+#else
         hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
         size_t tb = 0;
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
         void* t = ws->cub.ensure(tb);
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
         o.refs = dv.Current();
-        hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, dk.Current(), n, nb,
+        const uint32_t* sorted = dk.Current();
+#endif
+        hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, sorted, n, nb,
                            o.offs);
     }
     kp_end(32.0 * p.tot_sc + 4.0 * 8 * n, s);

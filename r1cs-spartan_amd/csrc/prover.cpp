@@ -10,6 +10,7 @@
 // full (HBM-streaming) and weights 1/G of the buckets; each MSM exchanges one XYZZ point per rank.
 // Every rank replays the same transcript, so no challenge broadcast.
 #include "prover.hpp"
+#include "sc_message.hpp"
 #include "pairing.hpp"
 
 #include <type_traits>
@@ -897,20 +898,6 @@ static void ser_open(Ser& s, const HFr& eval, const Affine<HFq2>& h, const std::
         host::g2_compress(b, p);
         s.raw(b, 96);
     }
-}
-
-// sumcheck #1 message from G(0), G(1), G(2): P(t) = C eq(tau_c, t) G(t), t = 0..L+2
-static std::vector<HFr> sc1_message(const HFr& Cc, const HFr& tau, const HFr g[3], int L) {
-    static const HFr inv2 = HFr::from_u64(2).inv();
-    std::vector<HFr> P(L + 3);
-    const HFr one = HFr::one(), two = HFr::from_u64(2);
-    for (int t = 0; t <= L + 2; ++t) {
-        HFr T = HFr::from_u64((uint64_t)t);
-        HFr l0 = (T - one) * (T - two) * inv2, l1 = T * (T - two), l2 = T * (T - one) * inv2;
-        HFr Gt = g[0] * l0 - g[1] * l1 + g[2] * l2;
-        P[t] = Cc * eq1(tau, T) * Gt;
-    }
-    return P;
 }
 
 // the quadratic through (0, g0), (1, g1), (2, g2) at t

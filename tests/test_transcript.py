@@ -20,3 +20,16 @@ def test_blake2s_kat_and_pieces(tmp_path):
                            os.path.join(ROOT, "tests", "native", "blake2s_check.cpp"), "-o", exe])
     out = subprocess.check_output([exe], timeout=120).decode()
     assert out.startswith("ok"), out
+
+
+def test_sumcheck1_message_stepping(tmp_path):
+    """prover.cpp's sumcheck-1 message (finite differences, sc_message.hpp) equals the point-by-point
+    Lagrange form of P(t) = C eq(tau, t) G(t) (prover.rs:199-207 with the degree-3 factorisation)"""
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if not cxx:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path / "scmsg")
+    subprocess.check_call([cxx, "-O2", "-std=c++17", "-w", "-I", os.path.join(ROOT, "r1cs-spartan_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "sc_message_check.cpp"), "-o", exe])
+    out = subprocess.check_output([exe], timeout=120).decode()
+    assert out.startswith("ok"), out

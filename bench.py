@@ -137,11 +137,13 @@ def oracle():
     return oc
 
 
-def cpu_baseline(kind, log_n, log_v, seconds_cap, threads=1, pp_bytes=None, stub=False, max_reps=3):
+def cpu_baseline(kind, log_n, log_v, seconds_cap, threads=1, pp_bytes=None, stub=False, max_reps=3, out_proof=None):
     """Test-oracle C prover (reference-faithful algorithms: log_n eq tables, degree-(log_n+2) sumcheck,
     hash-map eval_on_x, duplicated-scalar G2 MSMs, ark-ec Pippenger) on a bounded sample of the same
     workload: one thread (the reference is single-threaded as configured), or `threads` OpenMP
-    threads over the MSM windows and sumcheck pairs (what ark-ec's `parallel` feature would split)."""
+    threads over the MSM windows and sumcheck pairs (what ark-ec's `parallel` feature would split).
+    The proof of witness seed 0xB0B0 (FS transcript) is appended to `out_proof` when given: it is the
+    oracle's proof of the GPU's first witness, so the caller can compare the two byte for byte."""
     oc = oracle()
     inst = oc.Instance(kind, log_n, log_v, 0x5EED0000 + log_n, 0xB0B0 if kind == 3 else 0)
     pp = None if stub else (oc.PP.load(pp_bytes) if pp_bytes else oc.PP.keygen(log_n, 0xC0FFEE))
@@ -150,9 +152,11 @@ def cpu_baseline(kind, log_n, log_v, seconds_cap, threads=1, pp_bytes=None, stub
     try:
         while True:
             t0 = time.perf_counter()
-            oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, pp, 0, 0, commitment_stub=stub)
+            proof = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, pp, 0, 0, commitment_stub=stub)
             t_total += time.perf_counter() - t0
             reps += 1
+            if out_proof is not None and reps == 1:
+                out_proof.append(proof)
             if t_total >= seconds_cap or reps >= max_reps:
                 break
     finally:
@@ -374,6 +378,106 @@ def lvl0_for(g):
     return 1 if g >= 4 else 0
 
 
+def free_port():
+    import socket
+
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without an external launcher (WORLD_SIZE unset): start N rank processes
+    (this script again, one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment)
+    BEFORE this process makes any GPU call, wait for them, and re-print rank 0's JSON line. A rank that
+    fails ends the others (by their exact PIDs) and the launcher exits with its status. Nothing here
+    touches HIP, and no process is replaced (exec) by another."""
+    import tempfile
+
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            st = p.poll()
+            if st is None:
+                continue
+            live.remove(p)
+            if st != 0 and rc == 0:
+                rc = st if st > 0 else 128 - st
+                sys.stderr.write("bench.py launcher: rank %d exited with %d; stopping the others\n" % (procs.index(p), st))
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    if rc:
+        return rc
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.strip().startswith("{")]
+    if not lines:
+        sys.stderr.write("bench.py launcher: rank 0 printed no JSON line\n")
+        return 1
+    d = json.loads(lines[-1])
+    d["launcher"] = "bench.py --gpus %d: %d rank processes started by bench.py itself (no external launcher)" % (n, n)
+    print(json.dumps(d), flush=True)
+    return 0
+
+
+def init_dist(rank, world):
+    """gloo process group (rank 0's stdout is kept for its JSON line: rendezvous notices go to stderr)"""
+    import torch.distributed as dist
+
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+        dist.barrier()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
+def launch_only(rank, world, local):
+    """--launch-only: the rank reports what the launch gave it, with no HIP call (CPU test of the launcher)"""
+    seen = {"rank": rank, "local_rank": local, "world": world}
+    if os.environ.get("SPX_LAUNCH_TEST_FAIL") == str(rank):  # launcher test: this rank fails
+        sys.exit(3)
+    dist = init_dist(rank, world) if world > 1 else None
+    allseen = [seen]
+    if dist is not None:
+        allseen = [None] * world
+        dist.all_gather_object(allseen, seen)
+    if rank == 0:
+        print(json.dumps({"launch_only": True, "n_gpus": world, "ranks_seen": [s["world"] for s in allseen],
+                          "ranks": [s["rank"] for s in allseen], "local_ranks": [s["local_rank"] for s in allseen]}),
+              flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def comm_seen(ctx, rank, world):
+    """world size the context's product communicator actually spans: one allgather of every rank's id
+    on it (entries must come back in rank order)"""
+    got = ctx.comm_allgather(rank.to_bytes(4, "little"), world)
+    ids = [int.from_bytes(g, "little") for g in got]
+    if ids != list(range(world)):
+        raise RuntimeError("communicator returned rank ids %s, expected 0..%d" % (ids, world - 1))
+    return len(ids)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -405,35 +509,32 @@ def main():
     ap.add_argument("--rehearse", default="2,4,8",
                     help="N = 1: world sizes G for the one-rank rehearsal of a G-GPU proof-sharded node ('' to skip)")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
-                    help="N > 1 transport: on-node shared memory (default) or RCCL AllGather (one communicator per rank "
-                    "shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm)")
+                    help="N > 1 headline transport: on-node shared memory (default) or RCCL AllGather (one communicator "
+                    "per rank shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm). "
+                    "The other transport is measured beside it (value_comm_<other>) unless --one-comm")
+    ap.add_argument("--one-comm", action="store_true", help="N > 1: measure the headline transport only")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="start the ranks and report RANK / WORLD_SIZE without any HIP call (launcher test)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="proofs in flight per rank (worker contexts); default: 16 for unsharded and 2-rank proofs, "
                     "8 x G (at most 64) for proofs sharded over G >= 4 ranks (inflight_for)")
     ap.add_argument("--proofs-per-step", type=int, default=64,
                     help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's `python bench.py --gpus N`: this process becomes the launcher of N ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     stub = args.config == "c2"
     log_n = args.log_n or (18 if stub else 20)
     log_v = args.log_v
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        # the gloo rendezvous prints connection notices on stdout: keep stdout for rank 0's JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
-            dist.barrier()
-        finally:
-            sys.stdout.flush()
-            os.dup2(saved, 1)
-            os.close(saved)
+    if world != args.gpus and args.gpus != 1:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.launch_only:
+        return launch_only(rank, world, local)
+    dist = init_dist(rank, world) if world > 1 else None
 
     # host waits sleep rather than spin: with many proofs in flight the cores go to the transcript
     # hashing pool of spx_prove_many (measured: 31.2 vs 28.2 M constraints/s at 2^20 on one MI355X)
@@ -453,11 +554,9 @@ def main():
     need_batch = world == 1 or not sharded_head or not args.no_other
     need_sharded = world > 1 and (sharded_head or not args.no_other)
 
-    def make_sharded(k):
-        cs = [spx.Context(device) for _ in range(k)]
-        for c in cs:
-            c.set_lvl0_batch(lvl0_for(world))
-        if args.comm == "rccl":
+    def attach(cs, comm):
+        """put the sharded contexts on one transport; returns the RCCL hub (stats) or None"""
+        if comm == "rccl":
             # ONE communicator per rank; every proof in flight exchanges through its own channel of
             # the ordered hub (comm_hub.cpp), context j on channel j on every rank
             uid = [spx.comm_unique_id() if rank == 0 else None]
@@ -465,17 +564,28 @@ def main():
             hub = spx.ExchangeHub.rccl(uid[0], rank, world, device)
             for j, c in enumerate(cs):
                 c.set_comm_hub(hub, j)
-            hub.close()  # the contexts keep it alive
-        else:
-            name = [spx.shm_name() if rank == 0 else None]
-            dist.broadcast_object_list(name, src=0)
-            for j, c in enumerate(cs):
-                c.set_comm_shm("%s_%d" % (name[0], j), rank, world)
-        return cs
+            return hub
+        name = [spx.shm_name() if rank == 0 else None]
+        dist.broadcast_object_list(name, src=0)
+        for j, c in enumerate(cs):
+            c.set_comm_shm("%s_%d" % (name[0], j), rank, world)
+        return None
+
+    def make_sharded(k):
+        cs = [spx.Context(device) for _ in range(k)]
+        for c in cs:
+            c.set_lvl0_batch(lvl0_for(world))
+        return cs, attach(cs, args.comm)
 
     ctxs = [spx.Context(device) for _ in range(Bb)] if need_batch else []
-    sctxs = make_sharded(Bs) if need_sharded else []
+    sctxs, hub = make_sharded(Bs) if need_sharded else ([], None)
     ctx = (ctxs or sctxs)[0]
+    # the world size each rank's product communicator spans (one allgather of the rank ids on it)
+    seen = comm_seen(sctxs[0], rank, world) if sctxs else world
+    ranks_seen = [seen]
+    if dist is not None:
+        ranks_seen = [None] * world
+        dist.all_gather_object(ranks_seen, seen)
 
     n = 1 << log_n
     W = (args.witnesses or P) if args.kind == 3 else 1
@@ -570,6 +680,27 @@ def main():
             p4, el1 = timed(single_fn(octxs[0], opk))
             assert p4 == ref[0], "proof-sharded single proof differs"
         other = [el, el1]
+    # ---- N > 1: the same proof-sharded pipeline on the other transport (shm <-> RCCL over xGMI), so one
+    # run reports both. The contexts, index and witnesses stay; only their communicator changes.
+    xcomm = None
+    if sctxs and not args.one_comm:
+        alt = "rccl" if args.comm == "shm" else "shm"
+        if alt == "rccl" and os.environ.get("SPX_BENCH_SAME_GPU") == "1":
+            xcomm = {"comm": alt, "skipped": "every rank on GPU 0: RCCL refuses two ranks on one device"}
+        else:
+            hub_x = attach(sctxs, alt)
+            batch_fn(sctxs, spk, 1)()
+            px, elx = timed(batch_fn(sctxs, spk, args.steps))
+            check_batch(px, ref)
+            xcomm = {"comm": alt, "elapsed": elx}
+            if hub_x is not None:
+                xcomm["hub_stats_rank0"] = hub_x.stats()
+                hub_x.close()  # the contexts keep it alive
+    if hub is not None:
+        hub_stats = hub.stats()
+        hub.close()
+    else:
+        hub_stats = None
     # ---- N >= 4: proof groups (every proof sharded over K ranks, N / K groups side by side)
     grouped = {}
     if world >= 4 and not args.no_other and args.groups and not stub:
@@ -622,6 +753,7 @@ def main():
     ms_1 = elapsed_single / args.steps * 1e3
     ms_1c = elapsed_single_c / args.steps * 1e3 if elapsed_single_c else 0.0
     ms_o = ms_o1 = None
+    ms_x = xcomm["elapsed"] / args.steps * 1e3 if xcomm and "elapsed" in xcomm else 0.0
     ms_g = {}
     if dist is not None:
         import torch
@@ -630,12 +762,10 @@ def main():
             tg = torch.tensor([grouped[K] / args.steps * 1e3], dtype=torch.float64)
             dist.all_reduce(tg, op=dist.ReduceOp.MAX)
             ms_g[K] = float(tg[0])
-        import torch
-
         t = torch.tensor([ms, ms_c, ms_1, ms_1c, (other[0] / args.steps * 1e3) if other else 0.0,
-                          (other[1] / args.steps * 1e3) if other and other[1] else 0.0], dtype=torch.float64)
+                          (other[1] / args.steps * 1e3) if other and other[1] else 0.0, ms_x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, ms_c, ms_1, ms_1c = float(t[0]), float(t[1]), float(t[2]), float(t[3])
+        ms, ms_c, ms_1, ms_1c, ms_x = float(t[0]), float(t[1]), float(t[2]), float(t[3]), float(t[6])
         if other:
             ms_o, ms_o1 = float(t[4]), (float(t[5]) or None)
     # whole-job throughput: in batch mode every rank proves P proofs per step, sharded all ranks share them
@@ -662,7 +792,7 @@ def main():
                 wp = whole_proof_valu(ms / P)
                 if wp:
                     roof["whole_proof"] = wp
-    cpu = cpu_all = None
+    cpu = cpu_all = parity = None
     if world == 1 and not args.no_cpu:
         def gpu_pp_bytes(k):
             # the GPU keygen's PP (seed 0xC0FFEE, as the oracle's keygen would make it), loaded into the
@@ -679,9 +809,15 @@ def main():
                            pp_bytes=None if stub else gpu_pp_bytes(one_log_n))
         all_log_n = args.cpu_all_log_n if not stub else log_n
         pp_bytes = None if stub else gpu_pp_bytes(all_log_n)
+        oracle_proof = []
         cpu_all = cpu_baseline(args.kind, all_log_n, log_v, args.cpu_seconds, threads=host_cores(), pp_bytes=pp_bytes,
-                               stub=stub, max_reps=1)
+                               stub=stub, max_reps=1, out_proof=oracle_proof)
         del pp_bytes
+        if all_log_n == log_n and args.kind == 3 and args.mode == "fs" and oracle_proof:
+            # the oracle just proved witness 0xB0B0 under the same index and PP: the GPU's ref[0]
+            parity = oracle_proof[0] == ref[0]
+            if not parity:
+                sys.stderr.write("bench.py: PARITY FAILURE: the GPU proof differs from the oracle's at 2^%d\n" % log_n)
     wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
         KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
         "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
@@ -727,7 +863,21 @@ def main():
         "index_s": round(t_index, 2),
         "gen_s": round(t_gen, 2),
         "proof_bytes": len(ref[0]),
+        # the first witness's proof byte-equal to the test oracle's, proved in this run (cpu_baseline_all_cores)
+        "parity_2_%d" % log_n: parity,
+        "ranks_seen": ranks_seen,
     }
+    if xcomm is not None:
+        if "elapsed" in xcomm:
+            out["value_comm_%s" % xcomm["comm"]] = round(jobs * n / (ms_x / 1e3), 1)
+            out["ms_per_step_comm_%s" % xcomm["comm"]] = round(ms_x, 3)
+            if "hub_stats_rank0" in xcomm:
+                out["comm_%s_hub_stats_rank0" % xcomm["comm"]] = xcomm["hub_stats_rank0"]
+        else:
+            out["value_comm_%s" % xcomm["comm"]] = None
+            out["comm_%s_skipped" % xcomm["comm"]] = xcomm["skipped"]
+    if hub_stats is not None:
+        out["comm_%s_hub_stats_rank0" % args.comm] = hub_stats
     # host side: the machine's cores, the ones this process uses, and how many of them the per-proof
     # sequential Blake2s absorption of A, B, C keeps busy at the measured rate (proofs/s x seconds each)
     hash_s = phases.get("transcript_matrices", 0.0) / 1e6
@@ -802,8 +952,14 @@ def c2_line(spx, L, args, B):
         "roofline": roofline_hbm(stats, PMC_FILE_C2),
     }
     if not args.no_cpu:
+        op = []
         res["cpu_baseline_all_cores"] = cpu_baseline(3, log_n, log_v, args.cpu_seconds, threads=host_cores(), stub=True,
-                                                     max_reps=1)
+                                                     max_reps=1, out_proof=op)
+        if args.mode == "fs" and op:
+            # the oracle's stubbed proof of witness 0xB0B0 against the GPU's proof of the same witness
+            res["parity_2_18"] = op[0] == proofs[0]
+            if not res["parity_2_18"]:
+                sys.stderr.write("bench.py: PARITY FAILURE: the GPU C2 proof differs from the oracle's at 2^18\n")
     return res
 
 

@@ -93,8 +93,10 @@ int spx_comm_hub_create_group(void *group, int rank, void **hub_out);
 int spx_ctx_set_comm_hub(spx_ctx *ctx, void *hub, int channel);
 /* one exchange on `channel` without a context (transport tests); blocks until every rank posted it */
 int spx_comm_hub_allgather(void *hub, int channel, const void *send, void *recv, size_t bytes);
-/* out[0] control rounds, out[1] data rounds, out[2] exchanges served, out[3] largest batch per round */
-int spx_comm_hub_stats(void *hub, uint64_t out[4]);
+/* out[0] control rounds, out[1] data rounds, out[2] exchanges served, out[3] largest batch per round,
+ * out[4] idle rounds (matched nothing: a peer had not reached the exchange yet; each is followed by a
+ * 50 us back-off or the next local request) */
+int spx_comm_hub_stats(void *hub, uint64_t out[5]);
 int spx_comm_hub_destroy(void *hub); /* contexts attached keep the hub alive until they are destroyed */
 /* On-node shared-memory communicator (default for one process per GPU on one host): every rank
  * passes the same `name` (rank 0 makes it unique, e.g. "spx_<random hex>_<k>", and distributes it

@@ -92,6 +92,7 @@ EXPORTED = [
     "spx_comm_hub_stats",
     "spx_comm_hub_destroy",
     "spx_ctx_comm_allgather",
+    "spx_msm_reruns",
     "spx_pp_load",
     "spx_pp_generate",
     "spx_pp_serialize",
@@ -152,7 +153,10 @@ def lib():
     L.spx_comm_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.spx_comm_group_destroy.argtypes = [vp]
     L.spx_ctx_set_comm_group.argtypes = [vp, vp, ctypes.c_int]
-    L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    if hasattr(L, "spx_ctx_set_comm_rehearsal") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate it
+        L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    if hasattr(L, "spx_msm_reruns") or not os.environ.get("SPX_LIB_PATH"):
+        L.spx_msm_reruns.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
         L.spx_ctx_set_lvl0_batch.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_comm_hub_create_rccl") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate the hub
@@ -397,10 +401,11 @@ class ExchangeHub:
         return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(self.world)]
 
     def stats(self):
-        """control rounds, data rounds, exchanges served, largest batch in one round"""
-        out = (ctypes.c_uint64 * 4)()
+        """control rounds, data rounds, exchanges served, largest batch in one round, idle rounds (matched
+        nothing: a peer had not reached the exchange yet)"""
+        out = (ctypes.c_uint64 * 5)()
         _check(lib().spx_comm_hub_stats(self.h, out))
-        return dict(zip(("rounds", "data_rounds", "served", "max_batch"), list(out)))
+        return dict(zip(("rounds", "data_rounds", "served", "max_batch", "idle_rounds"), list(out)))
 
     def close(self):
         if self.h:

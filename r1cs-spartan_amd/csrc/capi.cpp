@@ -193,7 +193,7 @@ int spx_comm_hub_allgather(void* hub, int channel, const void* send, void* recv,
         spx::hub_allgather(**static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), channel, send, recv, bytes);
     });
 }
-int spx_comm_hub_stats(void* hub, uint64_t out[4]) {
+int spx_comm_hub_stats(void* hub, uint64_t out[5]) {
     return guard([&] {
         if (!hub || !out) spx::invalid("null argument");
         spx::hub_stats(**static_cast<std::shared_ptr<spx::OrderedHub>*>(hub), out);

@@ -15,6 +15,7 @@
 // request pending on one rank is matched by the same (channel, sequence) request of every other
 // rank, so no rank waits in a round its peers never reach.
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -40,7 +41,12 @@ struct OrderedHub {
     bool taken[kChannels] = {};
     bool stop = false;
     std::exception_ptr broken;  // a transport failure fails every later request too
-    uint64_t st_rounds = 0, st_data = 0, st_served = 0, st_max_batch = 0;
+    uint64_t st_rounds = 0, st_data = 0, st_served = 0, st_max_batch = 0, st_idle = 0;
+    uint64_t arrivals = 0;  // requests posted so far (a new one ends the back-off after an idle round)
+    // after a round that matched nothing, the hub waits this long (or for a new local request) before
+    // the next: peers reach their side of a pending exchange later, and an immediate next round would
+    // spin collectives (on RCCL a kernel plus a stream sync each) at full rate meanwhile
+    static constexpr auto kIdleBackoff = std::chrono::microseconds(50);
     std::vector<uint8_t> sbuf, rbuf;
     std::thread th;
 
@@ -74,6 +80,7 @@ struct OrderedHub {
         if (broken) std::rethrow_exception(broken);
         if (pend[ch]) invalid("two exchanges at once on one hub channel");
         pend[ch] = &q;
+        ++arrivals;
         cv_work.notify_one();
         cv_done.wait(lk, [&] { return q.done; });
         if (q.err) std::rethrow_exception(q.err);
@@ -93,6 +100,8 @@ struct OrderedHub {
     void run() {
         const int w = size();
         std::vector<uint32_t> ctl(kChannels), all((size_t)kChannels * w);
+        bool idle = false;       // the previous round matched nothing
+        uint64_t seen_arr = 0;   // arrivals at the previous round's snapshot
         for (;;) {
             Req* snap[kChannels];
             {
@@ -102,9 +111,11 @@ struct OrderedHub {
                         if (p) return true;
                     return false;
                 };
+                if (idle) cv_work.wait_for(lk, kIdleBackoff, [&] { return stop || arrivals != seen_arr; });
                 cv_work.wait(lk, [&] { return stop || any(); });
                 if (!any()) return;  // stop, nothing pending (peers have no request this rank lacks)
                 std::copy(pend, pend + kChannels, snap);
+                seen_arr = arrivals;
             }
             try {
                 for (int c = 0; c < kChannels; ++c) ctl[c] = snap[c] ? (uint32_t)(snap[c]->bytes + 1) : 0;
@@ -156,6 +167,8 @@ struct OrderedHub {
                 }
                 st_served += nm;
                 st_max_batch = std::max<uint64_t>(st_max_batch, nm);
+                idle = nm == 0;
+                st_idle += idle;
                 cv_done.notify_all();
             } catch (...) {
                 std::lock_guard<std::mutex> lk(mu);
@@ -187,12 +200,13 @@ void hub_allgather(OrderedHub& hub, int channel, const void* send, void* recv, s
     if (channel < 0 || channel >= OrderedHub::kChannels) invalid("hub channel out of range (0..63)");
     hub.allgather(channel, send, recv, bytes);
 }
-void hub_stats(OrderedHub& hub, uint64_t out[4]) {
+void hub_stats(OrderedHub& hub, uint64_t out[5]) {
     std::lock_guard<std::mutex> lk(hub.mu);
     out[0] = hub.st_rounds;
     out[1] = hub.st_data;
     out[2] = hub.st_served;
     out[3] = hub.st_max_batch;
+    out[4] = hub.st_idle;
 }
 
 }  // namespace spx

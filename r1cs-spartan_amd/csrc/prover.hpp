@@ -135,7 +135,7 @@ struct OrderedHub;
 std::shared_ptr<OrderedHub> make_hub(std::unique_ptr<Comm> base);
 std::unique_ptr<Comm> make_hub_channel(const std::shared_ptr<OrderedHub>& hub, int channel);
 void hub_allgather(OrderedHub& hub, int channel, const void* send, void* recv, size_t bytes);
-void hub_stats(OrderedHub& hub, uint64_t out[4]);  // rounds, data rounds, exchanges served, largest batch
+void hub_stats(OrderedHub& hub, uint64_t out[5]);  // rounds, data rounds, exchanges served, largest batch, idle rounds
 
 // ---------------------------------------------------------------- context
 struct Ctx {

@@ -53,7 +53,7 @@ MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
 KSYM = {"sc1_round": "k_sc1_wave<true, false, false>", "sc2_round": "k_sc2_wave<true, false, false>", "spmv3": "k_sparse3<0>",
-        "mtv3": "k_sparse3<1>", "open_level": "k_open_fold_wave<3>", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
+        "mtv3": "k_col_stream", "open_level": "k_open_fold_wave<3>", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
         "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq >", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
 KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
           "msm_accx_g1", "msm_accx_g2", "msm_reduce_g1", "msm_reduce_g2"]

@@ -23,6 +23,8 @@
  *   spx_sum_over_y       MatrixExtension::sum_over_y              src/data_structures/r1cs_reader.rs:75-85
  *   spx_eval_on_x        MatrixExtension::eval_on_x               src/data_structures/r1cs_reader.rs:91-117
  *   spx_msm_g1 / _g2     ark-ec VariableBaseMSM::multi_scalar_mul (called at commit.rs:25, open.rs:49)
+ *   spx_prover_*, spx_prove_*_round   the round-level prover API  src/ahp/prover.rs:109-281
+ *   spx_sumcheck_round   AHPForMLSumcheck::prove_round [linear-sumcheck] (called at prover.rs:204, 263)
  * Errors mirror src/error.rs:5-14 (Display is todo!() there; here a message string).
  */
 #ifndef SPARTAN_HIP_H
@@ -152,6 +154,38 @@ int spx_prove_witness(spx_ctx *ctx, spx_pk *idx, spx_witness *wit, spx_pp *pp, c
  * form of lib.rs:58-146 for a prover serving many witnesses; returns the first failure's status. */
 int spx_prove_many(spx_ctx **ctxs, int nctx, spx_pk *idx, spx_witness **wits, int nproofs, spx_pp *pp,
                    const spx_prove_opts *opts, uint8_t *out, size_t stride, size_t *lens);
+/* ---- round-level prover: the reference's interactive API (src/ahp/prover.rs:109-281), driven with
+ * verifier coins supplied by the caller as src/ahp/tests.rs:8-70 drives it. Each call takes the
+ * verifier message of its step (canonical Fr, 32 B each) and returns the prover message, ark-serialize
+ * compressed as the reference's message types (ProverFirstMessage .. ProverSixthMessage, the
+ * linear-sumcheck ProverMsg / IndexInfo). The session runs the same kernels as spx_prove: with the
+ * challenges a Fiat-Shamir prove would draw, the messages concatenate to spx_prove's proof (plus the
+ * two sumchecks' u64 round counts). One session or prove per context at a time.
+ *   spx_prover_init                  prover_init              prover.rs:109-121 (|v| power of two, |v|+|w| = n)
+ *   spx_prover_first_round           prover_first_round       prover.rs:123-141 (commitment)
+ *   spx_prover_second_round          prover_second_round      prover.rs:143-160 (r_v: log2|v| coins)
+ *   spx_prover_third_round           prover_third_round       prover.rs:163-196 (tau: log_n coins)
+ *   spx_prove_first_sumcheck_round   prove_first_sumcheck_round prover.rs:199-207 (NULL first, then r_{i-1})
+ *   spx_prove_fourth_round           prove_fourth_round       prover.rs:210-228 (last point of r_x)
+ *   spx_prove_fifth_round            prove_fifth_round        prover.rs:230-255 (r_a, r_b, r_c: 96 B)
+ *   spx_prove_second_sumcheck_round  prove_second_sumcheck_round prover.rs:258-266 (NULL first, then r_{i-1})
+ *   spx_prove_sixth_round            prove_sixth_round        prover.rs:268-281 (last point of r_y)
+ * Out-of-order calls fail with SPX_INVALID_ARGUMENT; a sumcheck round given a challenge first, or
+ * none later, or called past log_n rounds fails with SPX_SUMCHECK (linear-sumcheck's errors). */
+typedef struct spx_prover spx_prover;
+int spx_prover_init(spx_ctx *ctx, spx_pk *idx, const uint8_t *v, size_t nv, const uint8_t *w, size_t nw,
+                    spx_prover **out);
+int spx_prover_first_round(spx_prover *p, spx_pp *pp, uint8_t *msg, size_t cap, size_t *len);
+int spx_prover_second_round(spx_prover *p, const uint8_t *r_v, size_t n, spx_pp *pp, uint8_t *msg, size_t cap,
+                            size_t *len);
+int spx_prover_third_round(spx_prover *p, const uint8_t *tau, size_t n, uint8_t *msg, size_t cap, size_t *len);
+int spx_prove_first_sumcheck_round(spx_prover *p, const uint8_t *challenge, uint8_t *msg, size_t cap, size_t *len);
+int spx_prove_fourth_round(spx_prover *p, const uint8_t *last_point, uint8_t *msg, size_t cap, size_t *len);
+int spx_prove_fifth_round(spx_prover *p, const uint8_t *r_abc, uint8_t *msg, size_t cap, size_t *len);
+int spx_prove_second_sumcheck_round(spx_prover *p, const uint8_t *challenge, uint8_t *msg, size_t cap, size_t *len);
+int spx_prove_sixth_round(spx_prover *p, const uint8_t *last_point, spx_pp *pp, uint8_t *msg, size_t cap, size_t *len);
+int spx_prover_free(spx_prover *p);
+
 /* MLArgumentForR1CS::verify (src/lib.rs:147-212, verifier.rs:143-512): SPX_OK = accepted (the
  * reference's Ok(true)); a rejection returns the reference's error kind (SPX_INVALID_ARGUMENT,
  * SPX_SUMCHECK, SPX_WRONG_WITNESS, SPX_SERIALIZATION) with its message in spx_last_error.
@@ -238,6 +272,12 @@ int spx_msm_reruns(spx_ctx *ctx, uint64_t *reruns);
 /* ---- kernel-level entry points (parity tests) ---- */
 int spx_sum_over_y(spx_ctx *ctx, const spx_csr *m, const uint8_t *z, uint8_t *out);
 int spx_eval_on_x(spx_ctx *ctx, const spx_csr *m, const uint8_t *r_x, uint8_t *out);
+/* one AHPForMLSumcheck::prove_round [linear-sumcheck] of sum_b f(b) g(b) over n = 2^k canonical Fr
+ * (the second sumcheck's product shape, prover.rs:239-247): r_prev = NULL is the first round; with
+ * r_prev both tables are first bound at variable 0 to it (f_out / g_out receive the n / 2 bound
+ * entries, either may be NULL) and the round runs on the bound tables. evals_out = P(0), P(1), P(2). */
+int spx_sumcheck_round(spx_ctx *ctx, const uint8_t *f, const uint8_t *g, size_t n, const uint8_t *r_prev,
+                       uint8_t *evals_out, uint8_t *f_out, uint8_t *g_out);
 int spx_msm_g1(spx_ctx *ctx, const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out96);
 int spx_msm_g2(spx_ctx *ctx, const uint8_t *bases, const uint8_t *scalars, size_t n, uint8_t *out192);
 int spx_commit(spx_ctx *ctx, spx_pp *pp, const uint8_t *table, int nv, uint8_t *out56);

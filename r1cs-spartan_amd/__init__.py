@@ -118,6 +118,17 @@ EXPORTED = [
     "spx_verify",
     "spx_vp_from_pp",
     "spx_pairing_check",
+    "spx_prover_init",
+    "spx_prover_first_round",
+    "spx_prover_second_round",
+    "spx_prover_third_round",
+    "spx_prove_first_sumcheck_round",
+    "spx_prove_fourth_round",
+    "spx_prove_fifth_round",
+    "spx_prove_second_sumcheck_round",
+    "spx_prove_sixth_round",
+    "spx_prover_free",
+    "spx_sumcheck_round",
     "spx_sum_over_y",
     "spx_eval_on_x",
     "spx_msm_g1",
@@ -195,6 +206,19 @@ def lib():
     L.spx_cs_is_satisfied.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.spx_cs_matrices.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.spx_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    psz = ctypes.POINTER(sz)
+    if hasattr(L, "spx_prover_init") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate it
+        L.spx_prover_init.argtypes = [vp, vp, u8p, sz, u8p, sz, ctypes.POINTER(vp)]
+        L.spx_prover_first_round.argtypes = [vp, vp, ctypes.c_void_p, sz, psz]
+        L.spx_prover_second_round.argtypes = [vp, u8p, sz, vp, ctypes.c_void_p, sz, psz]
+        L.spx_prover_third_round.argtypes = [vp, u8p, sz, ctypes.c_void_p, sz, psz]
+        L.spx_prove_first_sumcheck_round.argtypes = [vp, u8p, ctypes.c_void_p, sz, psz]
+        L.spx_prove_fourth_round.argtypes = [vp, u8p, ctypes.c_void_p, sz, psz]
+        L.spx_prove_fifth_round.argtypes = [vp, u8p, ctypes.c_void_p, sz, psz]
+        L.spx_prove_second_sumcheck_round.argtypes = [vp, u8p, ctypes.c_void_p, sz, psz]
+        L.spx_prove_sixth_round.argtypes = [vp, u8p, vp, ctypes.c_void_p, sz, psz]
+        L.spx_prover_free.argtypes = [vp]
+        L.spx_sumcheck_round.argtypes = [vp, u8p, u8p, sz, u8p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.spx_sum_over_y.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
     L.spx_eval_on_x.argtypes = [vp, ctypes.POINTER(_CCsr), u8p, ctypes.c_void_p]
     L.spx_msm_g1.argtypes = [vp, u8p, u8p, sz, ctypes.c_void_p]
@@ -567,6 +591,86 @@ class MLArgumentForR1CS:
         _check(lib().spx_verify(pk.ctx.h, pk.h, vb, len(vb) // 32, bytes(proof), len(proof), bytes(vp), len(vp),
                                 ctypes.byref(o)))
         return True
+
+
+class InteractiveProver:
+    """The reference's round-level prover (src/ahp/prover.rs:109-281) over spx_prover_*: construct
+    with MLArgumentForR1CS-style inputs (prover_init), then call the rounds in the reference's order
+    with the verifier messages (canonical ints or 32-byte strings); each returns the prover message
+    as ark-serialize compressed bytes. Challenges of the sumcheck rounds: None first, then the
+    previous round's challenge (AHPForMLSumcheck::prove_round)."""
+
+    _CAP = 1 << 16
+
+    def __init__(self, pk, v, w):
+        vb, wb = _as_bytes(v), _as_bytes(w)
+        h = ctypes.c_void_p()
+        _check(lib().spx_prover_init(pk.ctx.h, pk.h, vb, len(vb) // 32, wb, len(wb) // 32, ctypes.byref(h)))
+        self.pk, self.h = pk, h
+
+    def _call(self, fn, *args):
+        out = ctypes.create_string_buffer(self._CAP)
+        n = ctypes.c_size_t(0)
+        _check(fn(self.h, *args, out, self._CAP, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    @staticmethod
+    def _one(x):
+        return None if x is None else _as_bytes([x] if isinstance(x, int) else x)
+
+    def prover_first_round(self, pp):
+        return self._call(lib().spx_prover_first_round, pp.h)
+
+    def prover_second_round(self, r_v, pp):
+        b = _as_bytes(r_v)
+        return self._call(lib().spx_prover_second_round, b, len(b) // 32, pp.h)
+
+    def prover_third_round(self, tau):
+        b = _as_bytes(tau)
+        return self._call(lib().spx_prover_third_round, b, len(b) // 32)
+
+    def prove_first_sumcheck_round(self, challenge=None):
+        return self._call(lib().spx_prove_first_sumcheck_round, self._one(challenge))
+
+    def prove_fourth_round(self, last_random_point):
+        return self._call(lib().spx_prove_fourth_round, self._one(last_random_point))
+
+    def prove_fifth_round(self, r_a, r_b, r_c):
+        return self._call(lib().spx_prove_fifth_round, _as_bytes([r_a, r_b, r_c]))
+
+    def prove_second_sumcheck_round(self, challenge=None):
+        return self._call(lib().spx_prove_second_sumcheck_round, self._one(challenge))
+
+    def prove_sixth_round(self, last_random_point, pp):
+        return self._call(lib().spx_prove_sixth_round, self._one(last_random_point), pp.h)
+
+    def close(self):
+        if self.h:
+            lib().spx_prover_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def sumcheck_round(ctx, f, g, r_prev=None):
+    """One AHPForMLSumcheck::prove_round of sum_b f(b) g(b) (spx_sumcheck_round): returns
+    ([P(0), P(1), P(2)] as 32-byte strings, f', g') with f', g' the tables bound to r_prev (None in
+    the first round)."""
+    fb, gb = _as_bytes(f), _as_bytes(g)
+    n = len(fb) // 32
+    ev = ctypes.create_string_buffer(96)
+    fo = ctypes.create_string_buffer(max(16 * n, 1))
+    go = ctypes.create_string_buffer(max(16 * n, 1))
+    rb = None if r_prev is None else _as_bytes([r_prev] if isinstance(r_prev, int) else r_prev)
+    _check(lib().spx_sumcheck_round(ctx.h, fb, gb, n, rb, ev, fo, go))
+    evals = [ev.raw[32 * k : 32 * k + 32] for k in range(3)]
+    if r_prev is None:
+        return evals, None, None
+    return evals, fo.raw[: 16 * n], go.raw[: 16 * n]
 
 
 class _Lc(ctypes.Structure):

@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "interactive.hpp"
 #include "pairing.hpp"
 #include "prover.hpp"
 
@@ -32,6 +33,10 @@ struct spx_pk {
 struct spx_witness {
     spx_ctx* ctx;
     std::unique_ptr<spx::Witness> w;
+};
+struct spx_prover {
+    spx_ctx* ctx;
+    std::unique_ptr<spx::Interactive> s;
 };
 
 namespace {
@@ -92,6 +97,18 @@ int copy_out(const std::vector<uint8_t>& v, uint8_t* out, size_t cap, size_t* le
         memcpy(out, v.data(), v.size());
     }
     return 0;
+}
+template <class F>
+int prover_step(spx_prover* p, uint8_t* msg, size_t cap, size_t* len, F&& f) {
+    return guard([&] {
+        if (!p) spx::invalid("null prover");
+        set_dev(p->ctx);
+        copy_out(f(*p->s), msg, cap, len);
+    });
+}
+spx::PP* need_pp(spx_pp* pp) {
+    if (!pp) spx::invalid("null public parameter");
+    return pp->p.get();
 }
 }  // namespace
 
@@ -299,6 +316,49 @@ int spx_prove(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uint
         copy_out(spx::prove(*ctx->c, *idx->i, *W, P, o), out, cap, len);
     });
 }
+// ---- round-level prover (interactive.cpp; prover.rs:109-281)
+int spx_prover_init(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw,
+                    spx_prover** out) {
+    return guard([&] {
+        set_dev(ctx);
+        if (!idx || !out) spx::invalid("null prover key / out");
+        if (!spx::is_pow2(nv)) spx::invalid("public input should be power of two");  // prover.rs:114-116
+        if (nv + nw != idx->i->n) spx::invalid("|v| + |w| != number of variables");  // prover.rs:117-119
+        auto W = spx::witness_upload(*ctx->c, v, nv, w, nw);
+        *out = new spx_prover{ctx, std::make_unique<spx::Interactive>(*ctx->c, *idx->i, std::move(W))};
+    });
+}
+int spx_prover_free(spx_prover* p) {
+    return guard([&] { delete p; });
+}
+int spx_prover_first_round(spx_prover* p, spx_pp* pp, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.first_round(need_pp(pp)); });
+}
+int spx_prover_second_round(spx_prover* p, const uint8_t* r_v, size_t n, spx_pp* pp, uint8_t* msg, size_t cap,
+                            size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.second_round(r_v, n, need_pp(pp)); });
+}
+int spx_prover_third_round(spx_prover* p, const uint8_t* tau, size_t n, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.third_round(tau, n); });
+}
+int spx_prove_first_sumcheck_round(spx_prover* p, const uint8_t* challenge, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len,
+                       [&](spx::Interactive& s) { return s.sumcheck_round(spx::Interactive::kSumcheck1, challenge); });
+}
+int spx_prove_fourth_round(spx_prover* p, const uint8_t* last_point, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.fourth_round(last_point); });
+}
+int spx_prove_fifth_round(spx_prover* p, const uint8_t* r_abc, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.fifth_round(r_abc); });
+}
+int spx_prove_second_sumcheck_round(spx_prover* p, const uint8_t* challenge, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len,
+                       [&](spx::Interactive& s) { return s.sumcheck_round(spx::Interactive::kSumcheck2, challenge); });
+}
+int spx_prove_sixth_round(spx_prover* p, const uint8_t* last_point, spx_pp* pp, uint8_t* msg, size_t cap, size_t* len) {
+    return prover_step(p, msg, cap, len, [&](spx::Interactive& s) { return s.sixth_round(last_point, need_pp(pp)); });
+}
+
 int spx_prove_witness(spx_ctx* ctx, spx_pk* idx, spx_witness* wit, spx_pp* pp, const spx_prove_opts* opts,
                       uint8_t* out, size_t cap, size_t* len) {
     return guard([&] {
@@ -518,6 +578,14 @@ int spx_eval_on_x(spx_ctx* ctx, const spx_csr* m, const uint8_t* r_x, uint8_t* o
         set_dev(ctx);
         auto r = spx::k_eval_on_x(*ctx->c, to_host(m), r_x);
         memcpy(out, r.data(), r.size());
+    });
+}
+int spx_sumcheck_round(spx_ctx* ctx, const uint8_t* f, const uint8_t* g, size_t n, const uint8_t* r_prev,
+                       uint8_t* evals_out, uint8_t* f_out, uint8_t* g_out) {
+    return guard([&] {
+        set_dev(ctx);
+        if (!f || !g || !evals_out) spx::invalid("null argument");
+        spx::k_sumcheck_round(*ctx->c, f, g, n, r_prev, evals_out, f_out, g_out);
     });
 }
 int spx_msm_g1(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out96) {

@@ -229,6 +229,56 @@ __global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* 
     }
 }
 
+// eval_on_x over the column stream (kernels.hpp: ColStreamView). One block of 4 waves per window of
+// 64 x spw columns; wave w takes slices w, w + 4, ... of its window (sorted by length, so the waves of
+// a block get similar totals). Lane l of a slice owns one column: its entries sit at off + 64 j + l,
+// so every step's loads are lane-contiguous, and a lane idles only for the steps between its own
+// length and the slice's longest column. out[y] = sum over the column's entries of
+// scale[m] * val * eq[row]; the window's columns are written by one block (one XCD's L2 merges them).
+DEV Fr sel3(uint32_t m, const Fr& a, const Fr& b, const Fr& c) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = m == 0 ? a.v[i] : (m == 1 ? b.v[i] : c.v[i]);
+    return r;
+}
+__global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, const Fr* __restrict__ eq, Fr* __restrict__ out,
+                                                         const Fr* __restrict__ scale) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const Fr s0 = ld_fr(scale), s1 = ld_fr(scale + 1), s2 = ld_fr(scale + 2);
+    for (uint32_t k = wid; k < cv.spw; k += kThreads / 64) {
+        const uint32_t si = blockIdx.x * cv.spw + k;
+        if (si >= cv.nslices) break;
+        const ColSlice sl = cv.slices[si];
+        const uint32_t info = cv.lanes[(size_t)si * 64 + lane];
+        const uint32_t len = info == kColNone ? 0u : info >> 26;
+        Fr acc;
+        fe_zero(acc);
+        const uint32_t* rp = cv.rowm + sl.off + lane;
+        const Fr* vp = cv.val + sl.off + lane;
+        uint32_t j = 0;
+        // two steps at a time: both entries' loads are in flight before the first product
+        for (; j + 1 < len; j += 2) {
+            const uint32_t r0 = rp[(size_t)j * 64], r1 = rp[(size_t)(j + 1) * 64];
+            Fr v0 = ld_fr(vp + (size_t)j * 64), v1 = ld_fr(vp + (size_t)(j + 1) * 64);
+            Fr q0 = ld_fr(eq + (r0 & 0x3FFFFFFFu)), q1 = ld_fr(eq + (r1 & 0x3FFFFFFFu)), t0, t1;
+            fe_mul(t0, v0, q0);
+            fe_mul(t1, v1, q1);
+            fe_mul(t0, t0, sel3(r0 >> 30, s0, s1, s2));
+            fe_mul(t1, t1, sel3(r1 >> 30, s0, s1, s2));
+            fe_add(acc, acc, t0);
+            fe_add(acc, acc, t1);
+        }
+        if (j < len) {
+            const uint32_t r0 = rp[(size_t)j * 64];
+            Fr v0 = ld_fr(vp + (size_t)j * 64), q0 = ld_fr(eq + (r0 & 0x3FFFFFFFu)), t0;
+            fe_mul(t0, v0, q0);
+            fe_mul(t0, t0, sel3(r0 >> 30, s0, s1, s2));
+            fe_add(acc, acc, t0);
+        }
+        if (info != kColNone) st_fr(out + (info & 0x3FFFFFFu), acc);
+    }
+}
+
 // Long rows: one block per chunk of <= kChunk entries; partial[chunk] = sum val * vec[idx].
 __global__ __launch_bounds__(kThreads) void k_sparse_chunks(SparseView3 mv, const Fr* __restrict__ vec,
                                                             const LongChunk* __restrict__ chunks,
@@ -961,6 +1011,20 @@ void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* 
         else
             hipLaunchKernelGGL(k_sparse_long_finish<1>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, o0, o1, o2,
                                scale);
+    }
+}
+
+void launch_col_stream(const ColStreamView& cv, const Fr* eq, Fr* out, const Fr* scale, const SparseView3& lv,
+                       const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows, Fr* partial,
+                       hipStream_t s) {
+    if (cv.nslices) {
+        const uint32_t nwin = (cv.nslices + cv.spw - 1) / cv.spw;
+        hipLaunchKernelGGL(k_col_stream, dim3(nwin), dim3(kThreads), 0, s, cv, eq, out, scale);
+    }
+    if (nchunks > 0) {
+        hipLaunchKernelGGL(k_sparse_chunks, dim3(nchunks), dim3(kThreads), 0, s, lv, eq, chunks, partial);
+        hipLaunchKernelGGL(k_sparse_long_finish<1>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, out, nullptr,
+                           nullptr, scale);
     }
 }
 

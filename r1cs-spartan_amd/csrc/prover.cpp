@@ -67,8 +67,6 @@ uint8_t* Ctx::pin_at(size_t off, size_t bytes, size_t region) {
     return pin + off;
 }
 
-static inline int ilog2(uint64_t x) { return 63 - __builtin_clzll(x); }
-static inline bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 
 // ====================================================================== public parameters
 int window_bits_for(uint64_t size) {
@@ -451,6 +449,129 @@ static void build_csc(const HostCsr& M, uint64_t n, std::vector<uint64_t>& cp, s
         }
 }
 
+// The column stream of the rank-local columns [lo, lo + cnt) of (up to) three CSC matrices for
+// k_col_stream (kernels.hpp: ColStreamView). A column's entries are A's, then B's, then C's (rows
+// ascending); columns are sorted by entry count, longest first, inside windows of 64 spw columns and
+// dealt to the lanes of 64-column slices, so a wave's lanes run columns of nearly equal length (the
+// per-column loop left lanes of Poisson-length columns idle for most of a wave's steps). Columns with
+// more than kLongCol entries take the chunked long path instead.
+static void upload_cols(Ctx& C, DevColStream& D, const std::vector<uint64_t>* cps, const std::vector<uint32_t>* rws,
+                        const std::vector<uint8_t>* vals, uint64_t lo, uint64_t cnt, int* err_dev) {
+    std::vector<uint32_t> len(cnt);
+    std::vector<uint64_t> long_cols;
+    uint64_t live = 0;
+    for (uint64_t y = 0; y < cnt; ++y) {
+        uint64_t L = 0;
+        for (int m = 0; m < 3; ++m) L += cps[m][lo + y + 1] - cps[m][lo + y];
+        live += L;
+        len[y] = L > kLongCol ? 0u : (uint32_t)L;
+        if (L > kLongCol) long_cols.push_back(y);
+    }
+    D.entries = live;
+    // one block (4 waves) per window: the widest window (<= 16 slices) that still gives >= 512 blocks
+    uint32_t spw = 16;
+    while (spw > 4 && (cnt + 64 * spw - 1) / (64 * spw) < 512) spw >>= 1;
+    D.spw = spw;
+    const uint64_t win = 64ull * spw, nslices = (cnt + 63) / 64;
+    D.nslices = (uint32_t)nslices;
+    std::vector<ColSlice> sl(nslices);
+    std::vector<uint32_t> lanes(64 * nslices, kColNone);
+    std::vector<uint64_t> order;
+    uint64_t tot = 0;
+    for (uint64_t w0 = 0; w0 < cnt; w0 += win) {
+        const uint64_t wn = std::min(win, cnt - w0);
+        order.resize(wn);
+        for (uint64_t i = 0; i < wn; ++i) order[i] = w0 + i;
+        std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return len[a] > len[b]; });
+        for (uint64_t s0 = 0; s0 < wn; s0 += 64) {
+            const uint64_t si = (w0 + s0) / 64;
+            uint32_t mx = 0;
+            for (uint64_t l = 0; l < 64 && s0 + l < wn; ++l) {
+                const uint64_t y = order[s0 + l];
+                lanes[64 * si + l] = (uint32_t)y | (len[y] << 26);
+                mx = std::max(mx, len[y]);
+            }
+            sl[si].off = tot;
+            sl[si].len = mx;
+            tot += 64ull * mx;
+        }
+    }
+    std::vector<uint32_t> rowm(std::max<uint64_t>(tot, 1), 0);
+    std::vector<uint8_t> val(32 * std::max<uint64_t>(tot, 1), 0);
+    for (uint64_t si = 0; si < nslices; ++si)
+        for (uint64_t l = 0; l < 64; ++l) {
+            const uint32_t info = lanes[64 * si + l];
+            if (info == kColNone) continue;
+            const uint64_t y = info & 0x3FFFFFFu;
+            if (!len[y]) continue;
+            uint64_t j = 0;
+            for (uint32_t m = 0; m < 3; ++m)
+                for (uint64_t k = cps[m][lo + y]; k < cps[m][lo + y + 1]; ++k, ++j) {
+                    const uint64_t e = sl[si].off + 64 * j + l;
+                    rowm[e] = rws[m][k] | (m << 30);
+                    memcpy(&val[32 * e], &vals[m][32 * k], 32);
+                }
+        }
+    D.slices.alloc(sizeof(ColSlice) * std::max<uint64_t>(nslices, 1));
+    D.lanes.alloc(4 * std::max<uint64_t>(lanes.size(), 1));
+    D.rowm.alloc(4 * rowm.size());
+    D.val.alloc(val.size());
+    if (nslices) {
+        SPX_HIP(hipMemcpyAsync(D.slices.p, sl.data(), sizeof(ColSlice) * nslices, hipMemcpyHostToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(D.lanes.p, lanes.data(), 4 * lanes.size(), hipMemcpyHostToDevice, C.stream));
+    }
+    SPX_HIP(hipMemcpyAsync(D.rowm.p, rowm.data(), 4 * rowm.size(), hipMemcpyHostToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(D.val.p, val.data(), val.size(), hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(D.val.as<Fr>(), val.size() / 32, err_dev, C.stream);
+    C.sync();  // host vectors go out of scope
+    // long columns: per-matrix entry arrays holding only their entries, chunked (k_sparse_chunks)
+    std::vector<uint32_t> li[3];
+    std::vector<uint8_t> lvv[3];
+    std::vector<LongChunk> chunks;
+    std::vector<LongRow> lrows;
+    for (uint32_t m = 0; m < 3; ++m)
+        for (uint64_t y : long_cols) {
+            const uint64_t b = cps[m][lo + y], e = cps[m][lo + y + 1];
+            if (b == e) continue;
+            LongRow lr{};
+            lr.m = m;
+            lr.x = y;
+            lr.chunk_begin = (uint32_t)chunks.size();
+            const uint64_t base = li[m].size();
+            for (uint64_t k = 0; k < e - b; k += kChunk) {
+                LongChunk ch{};
+                ch.m = m;
+                ch.begin = base + k;
+                ch.end = base + std::min<uint64_t>(k + kChunk, e - b);
+                chunks.push_back(ch);
+            }
+            lr.chunk_end = (uint32_t)chunks.size();
+            lrows.push_back(lr);
+            li[m].insert(li[m].end(), rws[m].begin() + b, rws[m].begin() + e);
+            lvv[m].insert(lvv[m].end(), vals[m].begin() + 32 * b, vals[m].begin() + 32 * e);
+        }
+    DevSparse& L = D.longc;
+    for (int m = 0; m < 3; ++m) {
+        L.ptr[m].alloc(8);
+        L.idx[m].alloc(4 * std::max<size_t>(li[m].size(), 1));
+        L.val[m].alloc(std::max<size_t>(lvv[m].size(), 32));
+        if (!li[m].empty()) {
+            SPX_HIP(hipMemcpyAsync(L.idx[m].p, li[m].data(), 4 * li[m].size(), hipMemcpyHostToDevice, C.stream));
+            SPX_HIP(hipMemcpyAsync(L.val[m].p, lvv[m].data(), lvv[m].size(), hipMemcpyHostToDevice, C.stream));
+            launch_to_mont(L.val[m].as<Fr>(), li[m].size(), err_dev, C.stream);
+        }
+    }
+    L.nchunks = (int)chunks.size();
+    L.nlrows = (int)lrows.size();
+    if (L.nchunks) {
+        L.chunks.alloc(sizeof(LongChunk) * chunks.size());
+        L.lrows.alloc(sizeof(LongRow) * lrows.size());
+        SPX_HIP(hipMemcpyAsync(L.chunks.p, chunks.data(), sizeof(LongChunk) * chunks.size(), hipMemcpyHostToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(L.lrows.p, lrows.data(), sizeof(LongRow) * lrows.size(), hipMemcpyHostToDevice, C.stream));
+    }
+    C.sync();
+}
+
 static void feed_matrix(Blake2s& h, const HostCsr& m) {
     // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize },
     // streamed through a 64 KiB staging block (u64 lengths, then (32-byte Fr, u64 column) per entry)
@@ -517,15 +638,14 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
     }
     // columns (CSC, last entry of a repeated (x, y) kept) for eval_on_x
     for (int m = 0; m < 3; ++m) build_csc(mats[m], n, rps[m], cols[m], vals[m]);
-    upload_sparse(C, I->cols, rps, cols, vals, lo, nl, err.as<int>());
+    upload_cols(C, I->cols, rps, cols, vals, lo, nl, err.as<int>());
     {
-        double e_rows = 0, e_cols = 0;
-        for (int m = 0; m < 3; ++m) {
-            e_rows += (double)(mats[m].rp[lo + nl] - mats[m].rp[lo]);
-            e_cols += (double)(rps[m][lo + nl] - rps[m][lo]);
-        }
+        double e_rows = 0;
+        for (int m = 0; m < 3; ++m) e_rows += (double)(mats[m].rp[lo + nl] - mats[m].rp[lo]);
         I->rows_bytes = 68.0 * e_rows + 3.0 * 8.0 * nl + 3.0 * 32.0 * nl;  // 3 outputs
-        I->cols_bytes = 68.0 * e_cols + 3.0 * 8.0 * nl + 32.0 * nl;        // 1 combined output
+        // column stream: 32 B value + 4 B row|matrix + 32 B gathered eq per entry; 4 B lane word and
+        // one combined 32 B output per column
+        I->cols_bytes = 68.0 * (double)I->cols.entries + 4.0 * nl + 32.0 * nl;
     }
     int herr = 0;
     SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
@@ -954,7 +1074,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
                           + n                // eq(r_x)
                           + nl + n2 + n4     // Mrx + fold
                           + n2 + n4          // z fold
-                          + std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.nchunks))
+                          + std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks))
                           + 8192 * 2 + 64 + 8 * L;  // partials, eq scratch, challenges
     C.scratch.ensure(32 * need);
     Fr* base = C.scratch.as<Fr>();
@@ -971,7 +1091,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Fr* EQ = take(n);
     Fr *M0 = take(nl), *M1 = take(n2), *M2 = take(n4);
     Fr *Z1 = take(n2), *Z2 = take(n4);
-    Fr* partial = take(std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.nchunks)));
+    Fr* partial = take(std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks)));
     Fr *eqlo = take(8192), *eqhi = take(8192);
     Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
     uint8_t* hp = C.pin_at(Ctx::kPinHp, 1 << 16, 64 << 10);
@@ -1018,11 +1138,13 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     if (!o.stub) commit_launch(C, *P, z, n, sh);
     if (early0) lvl0_launch(C, *P, z, L, sh);
     if (side0) lvl0_launch(C, *P, z, L, sh, true);
-    Transcript T(o.mode == 1, o.seed);
+    Transcript T(o.mode == 1, o.seed, o.coins);
     const uint64_t ctr = C.prove_seq++;
     const uint64_t seq = o.seq >= 0 ? (uint64_t)o.seq : ctr;
     const Blake2s* absorbed = o.await_absorbed ? o.await_absorbed() : o.absorbed;
-    if (o.cached && I.has_cache)
+    if (o.coins) {
+        // interactive: the caller is the verifier; nothing is absorbed
+    } else if (o.cached && I.has_cache)
         T.set_state(I.cache);
     else if (G == 1) {
         T.set_state(absorbed ? *absorbed : absorb_matrices(I));
@@ -1042,7 +1164,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         Ser s;
         s.u64(nvv);
         s.raw(W.v.data(), W.v.size());
-        T.feed(s.b.data(), s.b.size());
+        T.absorb(s.b.data(), s.b.size());
     }
     mark("transcript_matrices", tp);
     Affine<HFq> com = o.stub ? Affine<HFq>{HFq::zero(), HFq::zero(), true} : commit_finish(C, *P, z, n, comm);
@@ -1211,10 +1333,8 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     SPX_HIP(hipMemcpyAsync(rxdev, hp, 32 * (L + 3), hipMemcpyHostToDevice, C.stream));
     launch_eq_table(rxdev, L, 0, n, EQ, eqlo, eqhi, C.stream);
     {
-        SparseView3 cv = I.cols.view();
         kp_begin(KP_MTV, C.stream);
-        launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, rxdev + L, nl, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
-                       I.cols.lrows.as<LongRow>(), I.cols.nlrows, partial, C.stream);
+        I.cols.launch(EQ, M0, rxdev + L, partial, C.stream);
         kp_end(I.cols_bytes, C.stream);
     }
     {
@@ -1492,7 +1612,7 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
                             const std::vector<HFr>& r_y) {
     const int L = I.log_n;
     const uint64_t n = I.n;
-    const uint64_t parts = std::max<uint64_t>(3 * 2048, (uint64_t)I.cols.nchunks);
+    const uint64_t parts = std::max<uint64_t>(3 * 2048, (uint64_t)I.cols.longc.nchunks);
     C.scratch.ensure(32 * (n + n + n / 2 + 2 + parts + 8192 * 2 + 4 * L + 8));
     Fr* base = C.scratch.as<Fr>();
     Fr *EQ = base, *M0 = EQ + n, *Mb = M0 + n, *partial = Mb + n / 2 + 2, *eqlo = partial + parts, *eqhi = eqlo + 8192;
@@ -1504,9 +1624,7 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
     memcpy(hs, hch.data(), 32 * hch.size());
     SPX_HIP(hipMemcpyAsync(ch, hs, 32 * hch.size(), hipMemcpyHostToDevice, C.stream));
     launch_eq_table(ch, L, 0, n, EQ, eqlo, eqhi, C.stream);
-    SparseView3 cv = I.cols.view();
-    launch_sparse3(1, cv, EQ, M0, nullptr, nullptr, ch + L, n, I.cols.chunks.as<LongChunk>(), I.cols.nchunks,
-                   I.cols.lrows.as<LongRow>(), I.cols.nlrows, partial, C.stream);
+    I.cols.launch(EQ, M0, ch + L, partial, C.stream);
     // fold at r_y (variable 0 = LSB): M0 -> EQ (as q scratch) / Mb ping-pong
     const Fr* rin = M0;
     Fr* bufs[2] = {Mb, M0};
@@ -1653,11 +1771,11 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     std::vector<uint64_t> rps[3] = {cp, std::vector<uint64_t>(n + 1, 0), std::vector<uint64_t>(n + 1, 0)};
     std::vector<uint32_t> cols[3] = {rows, {}, {}};
     std::vector<uint8_t> vv[3] = {vals, {}, {}};
-    DevSparse D;
+    DevColStream D;
     DevMem err(sizeof(int)), rx(32 * L + 96), eq(32 * n), out(32 * n * 2), part(32 * std::max(4096, 1)), lo(32 << 14),
         hi(32 << 14);
     SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
-    upload_sparse(C, D, rps, cols, vv, 0, n, err.as<int>());
+    upload_cols(C, D, rps, cols, vv, 0, n, err.as<int>());
     std::vector<uint8_t> hr(32 * L + 96, 0);
     memcpy(hr.data(), r_x, 32 * L);
     HFr one = HFr::one();
@@ -1667,10 +1785,9 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     SPX_HIP(hipMemcpyAsync(rx.p, hr.data(), hr.size(), hipMemcpyHostToDevice, C.stream));
     launch_to_mont(rx.as<Fr>(), L + 3, err.as<int>(), C.stream);
     launch_eq_table(rx.as<Fr>(), L, 0, n, eq.as<Fr>(), lo.as<Fr>(), hi.as<Fr>(), C.stream);
-    if (D.nchunks > 4096) part.alloc(32 * D.nchunks);
+    if (D.longc.nchunks > 4096) part.alloc(32 * D.longc.nchunks);
     Fr* o = out.as<Fr>();
-    launch_sparse3(1, D.view(), eq.as<Fr>(), o, nullptr, nullptr, rx.as<Fr>() + L, n, D.chunks.as<LongChunk>(),
-                   D.nchunks, D.lrows.as<LongRow>(), D.nlrows, part.as<Fr>(), C.stream);
+    D.launch(eq.as<Fr>(), o, rx.as<Fr>() + L, part.as<Fr>(), C.stream);
     launch_from_mont(o + n, o, n, C.stream);
     std::vector<uint8_t> res(32 * n);
     SPX_HIP(hipMemcpyAsync(res.data(), o + n, 32 * n, hipMemcpyDeviceToHost, C.stream));
@@ -1679,6 +1796,49 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     C.sync();
     if (herr) throw SpxError(kSerialization, "non-canonical field element");
     return res;
+}
+
+// One AHPForMLSumcheck::prove_round [upstream linear-sumcheck] of sum_b f(b) g(b) (the second sumcheck's
+// product shape [r_M M(r_x, .), z], prover.rs:239-247) through the product's round kernels: with r_prev
+// the tables are first bound at variable 0 (T'[b] = T[2b] + r (T[2b+1] - T[2b]), n/2 entries out), then
+// P(t) = sum_b f'(b, t) g'(b, t) at t = 0, 1, 2. Canonical bytes in and out.
+void k_sumcheck_round(Ctx& C, const uint8_t* f, const uint8_t* g, uint64_t n, const uint8_t* r_prev,
+                      uint8_t* evals_out, uint8_t* f_out, uint8_t* g_out) {
+    if (!is_pow2(n) || n < (r_prev ? 4u : 2u)) invalid("table size must be a power of two (>= 2, >= 4 with a challenge)");
+    const bool fold = r_prev != nullptr;
+    const uint64_t half = fold ? n / 4 : n / 2;
+    DevMem err(sizeof(int)), tabs(32 * 2 * n), outs(32 * (fold ? n : 2)), res(32 * 3 + 32 * n),
+        part(32 * kRoundPartials);
+    SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
+    Fr* F = tabs.as<Fr>();
+    Fr* Gt = F + n;
+    SPX_HIP(hipMemcpyAsync(F, f, 32 * n, hipMemcpyHostToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(Gt, g, 32 * n, hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(F, 2 * n, err.as<int>(), C.stream);
+    Fr r{};
+    if (fold) {
+        uint64_t c[4];
+        memcpy(c, r_prev, 32);
+        if (HFr::geq_p(c)) throw SpxError(kSerialization, "non-canonical challenge");
+        r = dev_fr(HFr::from_canon(c));
+    }
+    Fr* Fo = fold ? outs.as<Fr>() : nullptr;
+    Fr* Go = fold ? Fo + n / 2 : nullptr;
+    Fr* ev = res.as<Fr>();
+    launch_sc2_round(fold, F, Gt, Fo, Go, r, half, part.as<Fr>(), C.ticket, ev, true, C.stream);
+    Fr* canon = ev + 3;
+    launch_from_mont(canon, ev, 3, C.stream);
+    int herr = 0;
+    SPX_HIP(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, C.stream));
+    SPX_HIP(hipMemcpyAsync(evals_out, canon, 96, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    if (herr) throw SpxError(kSerialization, "non-canonical field element");
+    if (fold) {
+        launch_from_mont(canon, Fo, n, C.stream);  // f' then g' (n / 2 each, contiguous)
+        if (f_out) SPX_HIP(hipMemcpyAsync(f_out, canon, 16 * n, hipMemcpyDeviceToHost, C.stream));
+        if (g_out) SPX_HIP(hipMemcpyAsync(g_out, canon + n / 2, 16 * n, hipMemcpyDeviceToHost, C.stream));
+        C.sync();
+    }
 }
 
 std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t* scalars, size_t n) {

@@ -33,6 +33,8 @@ enum { kOk = 0, kInvalidArgument = 1, kSumcheck = 2, kWrongWitness = 3, kSeriali
     } while (0)
 
 inline void invalid(const std::string& m) { throw SpxError(kInvalidArgument, m); }
+inline int ilog2(uint64_t x) { return 63 - __builtin_clzll(x); }
+inline bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 
 // Largest supported log_n / nv. Bounded by the MSM references (31-bit point index: n x 16 window
 // copies < 2^31 up to n = 2^26) and by the eq-table scratch (two halves of <= 2^13 entries each).
@@ -247,11 +249,25 @@ struct DevSparse {  // rank-local block of 3 matrices (CSR rows or CSC columns)
         return v;
     }
 };
+struct DevColStream {  // rank-local columns of A, B, C for eval_on_x (kernels.hpp: ColStreamView)
+    DevMem slices, lanes, rowm, val;
+    uint32_t nslices = 0, spw = 4;
+    DevSparse longc;  // columns of more than kLongCol entries: per-matrix entry arrays + chunks
+    uint64_t entries = 0;  // live entries (algorithmic bytes)
+    ColStreamView view() const {
+        return ColStreamView{slices.as<ColSlice>(), lanes.as<uint32_t>(), rowm.as<uint32_t>(), val.as<Fr>(), nslices, spw};
+    }
+    void launch(const Fr* eq, Fr* out, const Fr* scale, Fr* partial, hipStream_t s) const {
+        launch_col_stream(view(), eq, out, scale, longc.view(), longc.chunks.as<LongChunk>(), longc.nchunks,
+                          longc.lrows.as<LongRow>(), longc.nlrows, partial, s);
+    }
+};
 struct Index {
     int log_n = 0;
     uint64_t n = 0;
     HostCsr m[3];
-    DevSparse rows, cols;  // local rows (SpMV), local columns (eval_on_x)
+    DevSparse rows;      // local rows (SpMV)
+    DevColStream cols;   // local columns (eval_on_x)
     bool has_cache = false;
     Blake2s cache;  // transcript state after feeding A, B, C
     double rows_bytes = 0, cols_bytes = 0;  // algorithmic bytes of one SpMV / eval_on_x pass (local)
@@ -275,6 +291,9 @@ struct ProveOpts {
     // or, when set, called once the challenge-independent device work (SpMV, commitment MSM, shared
     // level-0 opening MSM) is queued, and returns that absorption (waiting for it if needed)
     std::function<const Blake2s*()> await_absorbed;
+    // interactive prove (round-level API, interactive.cpp): messages out, verifier coins in; no
+    // Fiat-Shamir absorption at all
+    ExternalCoins* coins = nullptr;
 };
 // Blake2s state after absorbing A, B, C (lib.rs:61-64): the per-proof sequential host work
 Blake2s absorb_matrices(const Index& I);
@@ -306,6 +325,8 @@ void verify(Ctx& C, Index& I, const uint8_t* v, size_t nv, const uint8_t* proof,
 
 std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z);
 std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x);
+void k_sumcheck_round(Ctx& C, const uint8_t* f, const uint8_t* g, uint64_t n, const uint8_t* r_prev,
+                      uint8_t* evals_out, uint8_t* f_out, uint8_t* g_out);
 std::vector<uint8_t> k_msm(Ctx& C, bool g2, const uint8_t* bases, const uint8_t* scalars, size_t n);
 std::vector<uint8_t> k_commit(Ctx& C, PP& P, const uint8_t* table, int nv);
 std::vector<uint8_t> k_open(Ctx& C, PP& P, const uint8_t* table, int nv, const uint8_t* point);

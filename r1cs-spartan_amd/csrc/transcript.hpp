@@ -118,15 +118,35 @@ class Blake2s {
     size_t buflen_;
 };
 
+// The verifier of an interactive prove (the reference's round-level API, prover.rs:109-281 driven as
+// in ahp/tests.rs:8-70): every prover message goes to message(), every challenge comes from draw()
+// (a verifier coin supplied by the caller).
+struct ExternalCoins {
+    virtual ~ExternalCoins() = default;
+    virtual void message(const void* d, size_t n) = 0;
+    virtual host::Fr draw() = 0;
+};
+
 class Transcript {
    public:
-    explicit Transcript(bool injected = false, uint64_t seed = 0) : injected_(injected), sm_(seed) {}
+    explicit Transcript(bool injected = false, uint64_t seed = 0, ExternalCoins* ext = nullptr)
+        : injected_(injected), sm_(seed), ext_(ext) {}
+    // a prover message (lib.rs:74-129 feeds each one before the next challenge)
     void feed(const void* d, size_t n) {
-        if (!injected_) h_.update(d, n);
+        if (ext_)
+            ext_->message(d, n);
+        else if (!injected_)
+            h_.update(d, n);
     }
+    // absorption that is not a prover message (the public input v, lib.rs:65)
+    void absorb(const void* d, size_t n) {
+        if (!ext_ && !injected_) h_.update(d, n);
+    }
+    bool external() const { return ext_ != nullptr; }
     void set_state(const Blake2s& b) { h_ = b; }
     const Blake2s& state() const { return h_; }
     host::Fr rand_fr() {
+        if (ext_) return ext_->draw();
         if (injected_) return sm_fr();
         for (;;) {
             uint64_t l[4];
@@ -174,6 +194,7 @@ class Transcript {
     }
     bool injected_;
     uint64_t sm_;
+    ExternalCoins* ext_;
     Blake2s h_;
 };
 

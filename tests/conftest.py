@@ -16,6 +16,21 @@ sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")
     config.addinivalue_line("markers", "slow: longer CPU-only cases")
+    hb = os.environ.get("SPX_HEARTBEAT")
+    if hb:
+        # long single tests (the oracle proving 2^22 for ~2 min) print nothing meanwhile: a line every
+        # 20 s into this file shows a remote runner that the run is alive
+        import threading
+        import time
+
+        def beat():
+            t0 = time.time()
+            while True:
+                with open(hb, "a") as f:
+                    f.write("alive %.0f s\n" % (time.time() - t0))
+                time.sleep(20)
+
+        threading.Thread(target=beat, daemon=True).start()
 
 
 def load_product():

@@ -1,6 +1,7 @@
-"""BASELINE size (2^20 constraints, the bench workload: circuit-3n) through size-independent
-properties — the CPU oracle cannot prove at this size in test time, so the GPU proof is checked
-instead of compared (tests/fullsize_check.py):
+"""BASELINE size (2^20 constraints, the bench workload: circuit-3n):
+
+* byte equality with the C oracle's proof of the same witness under the same PP (the oracle on the
+  box's cores, ~30 s at 16: BASELINE C3 pinned byte for byte, /root/reference/src/lib.rs:58-146);
 
 * determinism across the product's execution modes: per-proof transcript, index-cached transcript,
   concurrent contexts (spx_prove_many) and 2 virtual ranks all give the same bytes;
@@ -34,6 +35,18 @@ def test_fullsize_2_20(spx, ctx, oc):
     wit = spx.Witness(ctx, zb[: 32 << log_v], zb[32 << log_v :])
     proof = spx.MLArgumentForR1CS.prove_witness(pk, wit, pp)
     assert len(proof) == 21272
+
+    # the oracle's proof of the same witness (seed 0xB0B0) under the same PP, byte for byte
+    inst = oc.Instance(3, log_n, log_v, 0x5EED0000 + log_n, 0xB0B0)
+    assert inst.z_bytes == zb
+    ppc = oc.PP.load(pp.serialize_uncompressed())
+    oc.set_threads(bench.host_cores())
+    try:
+        want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
+    finally:
+        oc.set_threads(1)
+    del ppc
+    assert want == proof, "GPU proof differs from the oracle's at 2^20"
     assert spx.MLArgumentForR1CS.prove_witness(pk, wit, pp, cached=True) == proof
     ctx2 = spx.Context(0)
     assert all(p == proof for p in spx.MLArgumentForR1CS.prove_many([ctx, ctx2], pk, [wit] * 3, pp))

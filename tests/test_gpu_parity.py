@@ -230,3 +230,54 @@ def test_prove_bit_exact_2_16(spx, ctx, oc):
     pk = spx.MLArgumentForR1CS.index(ctx, *mats)
     got = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
     assert got == oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
+
+
+def _with_long_columns(oc, M, seed, extra):
+    """M plus entries that make some columns long: column 0 (z[0] = 1, as real circuits use ONE) in
+    every row, and columns c in `extra` (c -> count) in `count` random rows each, so columns of the
+    eval_on_x stream cross the long-column threshold (kernels.hpp: kLongCol = 62 entries: 62 stays
+    short, 63 goes to the chunked path) and rows gain repeated columns too."""
+    rs = random.Random(seed)
+    rows = [list(r) for r in M.to_rows()]
+    n = len(rows)
+    for row in rows:
+        row.append((rs.randrange(R), 0))
+    for c, cnt in extra.items():
+        for x in rs.sample(range(n), cnt):
+            rows[x].insert(rs.randrange(len(rows[x]) + 1), (rs.randrange(R), c))
+    return oc.CsrMatrix.from_rows(rows)
+
+
+def _sparse_columns(oc, n, seed):
+    """a matrix whose entries fall in a few columns: most columns are empty"""
+    rs = random.Random(seed)
+    rows = [[(rs.randrange(R), rs.choice((1, 2, 3, n - 1)))] if rs.random() < 0.7 else [] for _ in range(n)]
+    return oc.CsrMatrix.from_rows(rows)
+
+
+@pytest.mark.parametrize("log_n", [7, 10, 13])
+def test_eval_on_x_long_and_empty_columns(spx, ctx, oc, log_n):
+    inst = oc.Instance(0, log_n, 3, 505 + log_n)
+    rs = random.Random(log_n)
+    r_x = b"".join(rs.randrange(R).to_bytes(32, "little") for _ in range(log_n))
+    n = 1 << log_n
+    mats = [_with_long_columns(oc, inst.mats[0], log_n, {5: 62, 7: 63, 9: min(n, 4500)}), _sparse_columns(oc, n, log_n)]
+    for M in mats:
+        P = spx.Csr(M.n, M.row_ptr, M.col, M.val)
+        assert spx.MatrixExtension.eval_on_x(ctx, P, r_x) == oc.eval_on_x(M, r_x)
+        assert spx.MatrixExtension.sum_over_y(ctx, P, inst.z_bytes) == oc.sum_over_y(M, inst.z_bytes)
+
+
+@pytest.mark.parametrize("mode", ["fs", "injected"])
+def test_prove_bit_exact_long_columns(spx, ctx, oc, mode):
+    """Full proofs whose matrices have long columns (chunked path) next to short and empty ones."""
+    log_n, log_v = 11, 3
+    inst = oc.Instance(0, log_n, log_v, 6000 + log_n)
+    mats_o = [_with_long_columns(oc, inst.mats[0], 1, {5: 62, 7: 63, 11: 300}),
+              _with_long_columns(oc, inst.mats[1], 2, {6: 100}), _sparse_columns(oc, 1 << log_n, 3)]
+    ppc = oc.PP.keygen(log_n, 6100)
+    pp = spx.PublicParameter.load(ctx, ppc.serialize())
+    pk = spx.MLArgumentForR1CS.index(ctx, *[spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in mats_o])
+    got = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp, mode=mode, seed=67)
+    want = oc.prove(mats_o, inst.v_bytes, inst.w_bytes, ppc, 1 if mode == "injected" else 0, 67)
+    assert got == want

@@ -22,7 +22,7 @@ for step in "$@"; do
   case "$name" in
     tests)
       # shellcheck disable=SC2086
-      timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+      SPX_HEARTBEAT="$O/${TAG}_heartbeat.log" timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$O/${TAG}_tests.log" 2>&1 || exit $? ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/${TAG}_smoke.log" 2>&1 || exit $? ;;

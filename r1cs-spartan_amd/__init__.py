@@ -105,6 +105,7 @@ EXPORTED = [
     "spx_prove",
     "spx_prove_witness",
     "spx_prove_many",
+    "spx_hash_stats",
     "spx_last_timings",
     "spx_cs_create",
     "spx_cs_free",
@@ -194,6 +195,8 @@ def lib():
     L.spx_prove_many.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, ctypes.POINTER(vp), ctypes.c_int, vp,
                                  ctypes.POINTER(_Opts), ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_verify.argtypes = [vp, vp, u8p, sz, u8p, sz, u8p, sz, ctypes.POINTER(_Opts)]
+    if hasattr(L, "spx_hash_stats") or not os.environ.get("SPX_LIB_PATH"):
+        L.spx_hash_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.spx_vp_from_pp.argtypes = [vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
     L.spx_pairing_check.argtypes = [u8p, u8p, sz, ctypes.POINTER(ctypes.c_int)]
     L.spx_cs_create.argtypes = [ctypes.POINTER(vp)]
@@ -441,6 +444,13 @@ class ExchangeHub:
             self.close()
         except Exception:
             pass
+
+
+def hash_stats():
+    """(seconds, proofs, lane width) of spx_prove_many's matrix absorption so far (process-wide)"""
+    out = (ctypes.c_uint64 * 3)()
+    _check(lib().spx_hash_stats(out))
+    return out[0] / 1e9, out[1], out[2]
 
 
 def shm_name():

@@ -4,6 +4,7 @@
 #include "../../include/spartan_hip.h"
 
 #include <atomic>
+#include <chrono>
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
@@ -41,6 +42,8 @@ struct spx_prover {
 
 namespace {
 thread_local std::string g_err;
+// host time spent absorbing A, B, C in spx_prove_many's hashing pools, and the proofs absorbed
+std::atomic<uint64_t> g_hash_ns{0}, g_hash_proofs{0};
 template <class F>
 int guard(F&& f) {
     try {
@@ -411,22 +414,33 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     std::condition_variable cv;
     std::atomic<size_t> next_job{0};
     std::string pool_err;
+    // A job absorbs A, B, C for `lanes` consecutive proofs at once: multi-buffer BLAKE2s, one proof's
+    // state per vector lane (blake2s_lanes.cpp; 16 lanes with AVX-512, 8 with AVX2). Every proof's
+    // transcript still absorbs the matrices itself (lib.rs:61-64); the lanes share the instructions.
+    const int lanes = std::max(1, spx::blake2s_lane_width());
+    using clk = std::chrono::steady_clock;
+    const size_t njobs = (owned.size() + lanes - 1) / lanes;
     auto hasher = [&] {
+        std::vector<spx::Blake2s> tmp(lanes);
         for (;;) {
             const size_t j = next_job.fetch_add(1);
-            if (j >= owned.size()) return;
-            Slot& sl = slots[owned[j]];
+            if (j >= njobs) return;
+            const size_t b = j * lanes, e = std::min(owned.size(), b + lanes);
             int st = 1;
             try {
-                sl.h = spx::absorb_matrices(*idx->i);
-            } catch (const std::exception& e) {
+                const auto t0 = clk::now();
+                spx::absorb_matrices_lanes(*idx->i, tmp.data(), (int)(e - b));
+                for (size_t i = b; i < e; ++i) slots[owned[i]].h = tmp[i - b];
+                g_hash_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
+                g_hash_proofs += e - b;
+            } catch (const std::exception& ex) {
                 std::lock_guard<std::mutex> lk(mu);
-                pool_err = e.what();
+                pool_err = ex.what();
                 st = 2;
             }
             {
                 std::lock_guard<std::mutex> lk(mu);
-                sl.state.store(st);
+                for (size_t i = b; i < e; ++i) slots[owned[i]].state.store(st);
             }
             cv.notify_all();
         }
@@ -441,7 +455,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     budget = std::max(1, budget);
     int nh = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
     if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
-    nh = std::min<int>(nh, (int)owned.size());
+    nh = std::min<int>(nh, (int)njobs);
     std::vector<std::thread> pool;
     for (int t = 0; t < nh; ++t) pool.emplace_back(hasher);
 
@@ -478,7 +492,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     for (int k = 1; k < nw; ++k) th.emplace_back(work, k);
     work(0);
     for (auto& t : th) t.join();
-    next_job.store(owned.size());  // stop a pool still running after a worker failure
+    next_job.store(njobs);  // stop a pool still running after a worker failure
     for (auto& t : pool) t.join();
     for (int k = 0; k < nw; ++k)
         if (st[k] != SPX_OK) {
@@ -487,6 +501,14 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
         }
     g_err.clear();
     return SPX_OK;
+}
+int spx_hash_stats(uint64_t out[3]) {
+    return guard([&] {
+        if (!out) spx::invalid("null argument");
+        out[0] = g_hash_ns.load();
+        out[1] = g_hash_proofs.load();
+        out[2] = (uint64_t)std::max(1, spx::blake2s_lane_width());
+    });
 }
 int spx_vp_from_pp(spx_pp* pp, uint8_t* out, size_t cap, size_t* len) {
     return guard([&] {

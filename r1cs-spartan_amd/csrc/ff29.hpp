@@ -72,56 +72,33 @@ DEV void f29_zero(F29& r) {
 }
 DEV void f29_one(F29& r) { f29_set(r, Q29::ONE); }
 
-// Each Montgomery column is summed in SPX_F29_CHAINS independent 64-bit chains (products dealt
-// round-robin, the m[k-1] p[1] product last), joined with the previous column's carry at the end:
-// the column's products do not wait for the previous column, and the dependent chain per
-// coefficient is short enough to hide the v_mad_u64_u32 latency at one wave per SIMD.
-#ifndef SPX_F29_CHAINS
-#define SPX_F29_CHAINS 1
-#endif
-
-// An empty asm on each chain's sum before the join: integer addition is associative, and without
-// the barrier LLVM's reassociation folds the NC chains back into one serial v_mad_u64_u32 chain
-// (the generated code is then identical to NC = 1).
+// Each Montgomery column is one 64-bit accumulator (<= 42 products < 2^58). Splitting a column into 2-4
+// independent chains was measured slower at two waves per SIMD: dependent-mad latency
+// is not what bounds the G2 kernels.
+// An empty asm on a partial sum: integer addition is associative, and without the barrier LLVM's
+// reassociation folds separately summed chains back into one serial v_mad_u64_u32 chain.
 DEV uint64_t f29_opaque(uint64_t x) {
     asm("" : "+v"(x));
     return x;
-}
-template <int NC>
-DEV uint64_t f29_join(const uint64_t (&ch)[NC], uint64_t carry) {
-    if constexpr (NC == 1) return ch[0] + carry;
-    else if constexpr (NC == 2) return (f29_opaque(ch[0]) + f29_opaque(ch[1])) + carry;
-    else if constexpr (NC == 3) return (f29_opaque(ch[0]) + f29_opaque(ch[1])) + (f29_opaque(ch[2]) + carry);
-    else return ((f29_opaque(ch[0]) + f29_opaque(ch[1])) + (f29_opaque(ch[2]) + f29_opaque(ch[3]))) + carry;
 }
 
 // REDC(sum of NP products a_j b_j): NP = 1 (f29_mul) or 2 (f29_mul2, lazy reduction)
 template <int NP>
 DEV void f29_redc_sum(F29& r, const F29* const (&a)[NP], const F29* const (&b)[NP]) {
-    constexpr int NC = SPX_F29_CHAINS;
     uint32_t m[14], t[14];
     uint64_t carry = 0;
 #pragma unroll
     for (int k = 0; k < 27; ++k) {
         const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
-        uint64_t ch[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) ch[c] = 0;
-        int j = 0;
+        uint64_t ch = 0;
 #pragma unroll
         for (int i = lo; i <= hi; ++i) {
 #pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                ch[j % NC] += (uint64_t)a[q]->v[i] * b[q]->v[k - i];
-                ++j;
-            }
+            for (int q = 0; q < NP; ++q) ch += (uint64_t)a[q]->v[i] * b[q]->v[k - i];
         }
 #pragma unroll
-        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) {
-            ch[j % NC] += (uint64_t)m[i] * Q29::P[k - i];
-            ++j;
-        }
-        uint64_t acc = f29_join<NC>(ch, carry);
+        for (int i = lo; i <= (k < 14 ? k - 1 : 13); ++i) ch += (uint64_t)m[i] * Q29::P[k - i];
+        uint64_t acc = ch + carry;
         if (k < 14) {
             m[k] = ((uint32_t)acc * Q29::PINV) & Q29::M;
             acc += (uint64_t)m[k] * Q29::P[0];

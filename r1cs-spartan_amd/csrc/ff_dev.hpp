@@ -181,14 +181,10 @@ DEV void fe_mul_cios(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
 
 template <class C>
 DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
-#ifdef SPX_NO_ASM_MUL
-    fe_mul_cios(r, a, b);
-#else
     if constexpr (C::N == 8)
         fr_mul_asm(r, a, b);
     else
         fq_mul_asm(r, a, b);
-#endif
 }
 
 template <class C>
@@ -240,25 +236,11 @@ DEV void fe_inv(Fe<C>& r, const Fe<C>& a) {
 }
 
 // ---------------------------------------------------------------- Fq2
-// G2 code calls Fq2 products out of line: a fully inlined G2 point addition is ~30 inlined 12-limb
-// Montgomery products (~25k instructions), which overflows the instruction cache. SPX_F2_MODE:
-//   0: each Fq product is a call (smallest code, no ILP across the Karatsuba products)
-//   1: each Fq2 product / square is a call; its 3 (2) Fq products are inline and independent,
-//      so one wave overlaps their multiply-accumulate chains (G2 kernels run at occupancy 1)
-//   2: everything inline
-#ifndef SPX_F2_MODE
-#define SPX_F2_MODE 1
-#endif
-#if SPX_F2_MODE == 0
-static __device__ __noinline__ Fq fq_mul_call(Fq a, Fq b) {
-    Fq r;
-    fe_mul(r, a, b);
-    return r;
-}
-#define SPX_FQMUL(r, a, b) (r) = fq_mul_call((a), (b))
-#else
+// 32-bit-limb Fq2 (the PP loading / keygen / verifier-side kernels; the MSM hot path uses the
+// radix-2^29 lane-pair form of fq2pair.hpp). Each Fq2 product / square is a call with its 3 (2) Fq
+// products inline and independent: a fully inlined G2 point addition is ~30 inlined 12-limb products
+// (~25k instructions), which overflows the instruction cache.
 #define SPX_FQMUL(r, a, b) fe_mul((r), (a), (b))
-#endif
 DEV void f2_zero(Fq2& r) {
     fe_zero(r.c0);
     fe_zero(r.c1);
@@ -301,7 +283,6 @@ DEV void f2_sqr_inl(Fq2& r, const Fq2& a) {
     SPX_FQMUL(r.c0, s, d);
     fe_add(r.c1, p, p);
 }
-#if SPX_F2_MODE == 1
 static __device__ __noinline__ Fq2 f2_mul_call(Fq2 a, Fq2 b) {
     Fq2 r;
     f2_mul_inl(r, a, b);
@@ -314,10 +295,6 @@ static __device__ __noinline__ Fq2 f2_sqr_call(Fq2 a) {
 }
 DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) { r = f2_mul_call(a, b); }
 DEV void f2_sqr(Fq2& r, const Fq2& a) { r = f2_sqr_call(a); }
-#else
-DEV void f2_mul(Fq2& r, const Fq2& a, const Fq2& b) { f2_mul_inl(r, a, b); }
-DEV void f2_sqr(Fq2& r, const Fq2& a) { f2_sqr_inl(r, a); }
-#endif
 DEV void f2_inv(Fq2& r, const Fq2& a) {
     Fq t0, t1, n;
     fe_sqr(t0, a.c0);

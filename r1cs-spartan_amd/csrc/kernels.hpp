@@ -31,11 +31,12 @@ struct LongRow {
     uint64_t x;  // local output index
 };
 // eval_on_x column stream (k_col_stream): the A, B, C entries of each column concatenated, columns
-// sorted by length inside windows of 64 x spw columns and dealt to the 64 lanes of a slice (SELL-64),
+// sorted by length inside windows of 64 x kColWindow columns and dealt to the 64 lanes of a slice (SELL-64),
 // so the lanes of a wave run columns of (nearly) equal length. Columns with more than kLongCol
 // entries go to the chunked long path (a lane's length is a 6-bit field).
 static constexpr uint32_t kLongCol = 62;
 static constexpr uint32_t kColNone = 0xFFFFFFFFu;  // lane slot without a column
+static constexpr uint32_t kColWindow = 16;         // slices per sorting window (1024 columns)
 struct ColSlice {
     uint64_t off;  // first entry slot of the slice: entry j of lane l at off + 64 j + l
     uint32_t len;  // the slice's longest column (steps)
@@ -46,7 +47,7 @@ struct ColStreamView {
     const uint32_t* lanes;   // [64 nslices]: local column | entries << 26, or kColNone
     const uint32_t* rowm;    // entry slots: row | matrix << 30
     const Fr* val;           // entry slots: Montgomery values
-    uint32_t nslices, spw;   // slices, slices per window (one window per block of 4 waves)
+    uint32_t nslices;
 };
 // per-block partial sums of one sumcheck round (3 Fr per block, up to 8192 blocks)
 static constexpr uint64_t kRoundPartials = 3 * 8192;
@@ -142,11 +143,22 @@ void launch_from_mont(Fr* out, const Fr* in, size_t n, hipStream_t s);
 void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* o1, Fr* o2, const Fr* scale,
                     uint64_t count, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
                     Fr* partial, hipStream_t s);
-// out[y] = sum_m scale[m] sum_x eq[x] M[x][y] over the column stream, then the long columns' chunks
-// (k_sparse_chunks over `lv`'s per-matrix entry arrays) added by k_sparse_long_finish<1>
-void launch_col_stream(const ColStreamView& cv, const Fr* eq, Fr* out, const Fr* scale, const SparseView3& lv,
-                       const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows, Fr* partial,
-                       hipStream_t s);
+// eq(r_x, .) over L variables as the product of nf tables over consecutive bit fields of x (variable
+// 0 = LSB): t[f] has 2^k[f] entries, the last one three copies scaled by r_A, r_B, r_C (m 2^k + x).
+// eq_factors_for: nf = 2 (k[0] = ceil(L / 2) <= 13)
+struct EqFactors {
+    const Fr* t[3];
+    int k[3];
+    int nf;
+};
+// the split used for L variables, tables carved from `scratch` (kEqScratch Fr)
+static constexpr uint64_t kEqScratch = 4 * 8192;
+EqFactors eq_factors_for(int L, Fr* scratch);
+// out[y] = sum_m scale[m] sum_x eq(r_x, x) M[x][y] over the column stream (r_x: L device Fr, scale: 3),
+// then the long columns' chunks (over `lv`'s per-matrix entry arrays) added in
+void launch_col_stream(const ColStreamView& cv, const Fr* r_x, int L, const Fr* scale, Fr* out, Fr* eq_scratch,
+                       const SparseView3& lv, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
+                       Fr* partial, hipStream_t s);
 void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* out, Fr* scratch_lo,
                      Fr* scratch_hi, hipStream_t s);
 int sc_grid(uint64_t half);

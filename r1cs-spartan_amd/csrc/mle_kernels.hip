@@ -27,20 +27,9 @@ DEV Fr ld_fr(const Fr* p) {
     return r;
 }
 DEV void st_fr(Fr* p, const Fr& v) { store_vec(p, v); }
-// folded sumcheck tables: written once, read by the next round (SPX_FOLD_NT=1: non-temporal stores)
-#ifndef SPX_FOLD_NT
-#define SPX_FOLD_NT 0
-#endif
+// folded sumcheck tables: written once, read by the next round (non-temporal stores measured no gain)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-DEV void st_fr_fold(Fr* p, const Fr& v) {
-    if constexpr (SPX_FOLD_NT) {
-        u32x4* d = reinterpret_cast<u32x4*>(p);
-        __builtin_nontemporal_store((u32x4){v.v[0], v.v[1], v.v[2], v.v[3]}, d);
-        __builtin_nontemporal_store((u32x4){v.v[4], v.v[5], v.v[6], v.v[7]}, d + 1);
-    } else {
-        store_vec(p, v);
-    }
-}
+DEV void st_fr_fold(Fr* p, const Fr& v) { store_vec(p, v); }
 
 // ------------------------------------------------------------------ block reduction of K Fr values
 template <int K>
@@ -229,24 +218,27 @@ __global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* 
     }
 }
 
-// eval_on_x over the column stream (kernels.hpp: ColStreamView). One block of 4 waves per window of
-// 64 x spw columns; wave w takes slices w, w + 4, ... of its window (sorted by length, so the waves of
-// a block get similar totals). Lane l of a slice owns one column: its entries sit at off + 64 j + l,
-// so every step's loads are lane-contiguous, and a lane idles only for the steps between its own
-// length and the slice's longest column. out[y] = sum over the column's entries of
-// scale[m] * val * eq[row]; the window's columns are written by one block (one XCD's L2 merges them).
-DEV Fr sel3(uint32_t m, const Fr& a, const Fr& b, const Fr& c) {
-    Fr r;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = m == 0 ? a.v[i] : (m == 1 ? b.v[i] : c.v[i]);
-    return r;
-}
-__global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, const Fr* __restrict__ eq, Fr* __restrict__ out,
-                                                         const Fr* __restrict__ scale) {
+// eval_on_x over the column stream (kernels.hpp: ColStreamView). eq(r_x, x) is never materialised:
+// it factors as lo[x & (2^klo - 1)] * hi[x >> klo] over the low and high variables (eq.rs:5-20 in
+// product form), with the matrix scale r_M folded into three copies of hi (EqFactors, nf = 2:
+// hi3[m << khi | x_hi] = r_M hi[x_hi]); the two tables (<= 2^13 entries each) stay in L2. An entry
+// then costs one streamed 36 B (value, row | matrix), two cache-resident gathers and two Montgomery
+// products, where a materialised n-entry table costs a random 32 B HBM gather plus the table's write.
+// One block of 4 waves per window of 16 slices of 64 columns sorted by length (the window's output
+// lines are written by one CU); wave w takes slices w, w + 4, w + 8, w + 12, so the waves of a block get
+// similar totals. Lane l of a slice owns one column: its entries sit at off + 64 j + l (lane-contiguous
+// loads per step), and a lane idles only for the steps between its own length and the slice's longest.
+// The kernel is bound by the dependent multiply-accumulate chains of the Montgomery products (VALU
+// latency: two entries per step give each wave two independent chains), not by HBM.
+__global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFactors ef, Fr* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const Fr s0 = ld_fr(scale), s1 = ld_fr(scale + 1), s2 = ld_fr(scale + 2);
-    for (uint32_t k = wid; k < cv.spw; k += kThreads / 64) {
-        const uint32_t si = blockIdx.x * cv.spw + k;
+    const Fr* __restrict__ lo = ef.t[0];
+    const Fr* __restrict__ hi3 = ef.t[1];
+    const int klo = ef.k[0], khi = ef.k[1];
+    const uint32_t mask = (1u << klo) - 1;
+    auto hidx = [&](uint32_t rm) { return ((rm >> 30) << khi) | ((rm & 0x3FFFFFFFu) >> klo); };
+    for (uint32_t k = wid; k < kColWindow; k += kThreads / 64) {
+        const uint32_t si = blockIdx.x * kColWindow + k;
         if (si >= cv.nslices) break;
         const ColSlice sl = cv.slices[si];
         const uint32_t info = cv.lanes[(size_t)si * 64 + lane];
@@ -256,27 +248,52 @@ __global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, const
         const uint32_t* rp = cv.rowm + sl.off + lane;
         const Fr* vp = cv.val + sl.off + lane;
         uint32_t j = 0;
-        // two steps at a time: both entries' loads are in flight before the first product
+        // two entries at a time: both entries' loads are in flight before the first product, and the
+        // two products are independent chains
         for (; j + 1 < len; j += 2) {
             const uint32_t r0 = rp[(size_t)j * 64], r1 = rp[(size_t)(j + 1) * 64];
             Fr v0 = ld_fr(vp + (size_t)j * 64), v1 = ld_fr(vp + (size_t)(j + 1) * 64);
-            Fr q0 = ld_fr(eq + (r0 & 0x3FFFFFFFu)), q1 = ld_fr(eq + (r1 & 0x3FFFFFFFu)), t0, t1;
-            fe_mul(t0, v0, q0);
-            fe_mul(t1, v1, q1);
-            fe_mul(t0, t0, sel3(r0 >> 30, s0, s1, s2));
-            fe_mul(t1, t1, sel3(r1 >> 30, s0, s1, s2));
+            Fr a0 = ld_fr(lo + (r0 & mask)), a1 = ld_fr(lo + (r1 & mask));
+            Fr b0 = ld_fr(hi3 + hidx(r0)), b1 = ld_fr(hi3 + hidx(r1)), t0, t1;
+            fe_mul(t0, v0, a0);
+            fe_mul(t1, v1, a1);
+            fe_mul(t0, t0, b0);
+            fe_mul(t1, t1, b1);
             fe_add(acc, acc, t0);
             fe_add(acc, acc, t1);
         }
         if (j < len) {
             const uint32_t r0 = rp[(size_t)j * 64];
-            Fr v0 = ld_fr(vp + (size_t)j * 64), q0 = ld_fr(eq + (r0 & 0x3FFFFFFFu)), t0;
-            fe_mul(t0, v0, q0);
-            fe_mul(t0, t0, sel3(r0 >> 30, s0, s1, s2));
+            Fr v0 = ld_fr(vp + (size_t)j * 64), a0 = ld_fr(lo + (r0 & mask)), b0 = ld_fr(hi3 + hidx(r0)), t0;
+            fe_mul(t0, v0, a0);
+            fe_mul(t0, t0, b0);
             fe_add(acc, acc, t0);
         }
         if (info != kColNone) st_fr(out + (info & 0x3FFFFFFu), acc);
     }
+}
+
+// long columns: one block per chunk of <= kChunk entries of one matrix; partial[chunk] = sum over the
+// chunk of val * eq(r_x, row) * r_m, the factor tables read from global memory (EqFactors)
+__global__ __launch_bounds__(kThreads) void k_col_chunks(SparseView3 mv, EqFactors ef, const LongChunk* __restrict__ chunks,
+                                                         Fr* __restrict__ partial) {
+    const LongChunk ch = chunks[blockIdx.x];
+    const Fr* val = mv.val[ch.m];
+    const uint32_t* idx = mv.idx[ch.m];
+    const int last = ef.nf - 1;
+    Fr acc[1];
+    fe_zero(acc[0]);
+    for (uint64_t k = ch.begin + threadIdx.x; k < ch.end; k += blockDim.x) {
+        uint32_t r = idx[k];
+        Fr t = ld_fr(val + k);
+        for (int f = 0; f < ef.nf; ++f) {
+            const uint32_t i = f == last ? ((uint32_t)ch.m << ef.k[f]) | r : r & ((1u << ef.k[f]) - 1);
+            fe_mul(t, t, ld_fr(ef.t[f] + i));
+            r >>= ef.k[f];
+        }
+        fe_add(acc[0], acc[0], t);
+    }
+    block_reduce_store<1>(acc, partial + blockIdx.x);
 }
 
 // Long rows: one block per chunk of <= kChunk entries; partial[chunk] = sum val * vec[idx].
@@ -322,29 +339,61 @@ __global__ void k_sparse_long_finish(const LongRow* __restrict__ rows, int nrows
 }
 
 // ------------------------------------------------------------------ eq tables
-// One block: tab[x] = prod_{j<k} eq(r_j, x_j) for x < 2^k (k <= 12), variable 0 = LSB.
-__global__ __launch_bounds__(kThreads) void k_eq_small(const Fr* __restrict__ r, int k, Fr* __restrict__ tab) {
-    if (threadIdx.x == 0) {
-        Fr one;
-        fe_one(one);
-        st_fr(tab, one);
+// eq tables of <= 13 variables, variable 0 = LSB: tab[x] = prod_{j<k} eq(r_j, x_j), eq(r, 1) = r,
+// eq(r, 0) = 1 - r (eq.rs:5-20). Block f builds the table of the f-th field of ef.k (variables
+// sum_{g<f} k_g ..) into ef.t[f]; the last block, if scale, writes the three scaled copies
+// scale[m] tab[x] at m 2^k + x instead. Each table is the outer product of two sub-tables of <= 7
+// variables computed directly in LDS (k / 2 + 1 dependent products deep, no per-variable barrier),
+// one product per output entry.
+static constexpr int kEqThreads = 1024;
+__global__ __launch_bounds__(kEqThreads) void k_eq_factors(const Fr* __restrict__ r, EqFactors ef,
+                                                           const Fr* __restrict__ scale) {
+    __shared__ Fr A[64], B[128 * 3];
+    const int f = blockIdx.x;
+    const int k = ef.k[f];
+    int off = 0;
+    for (int g = 0; g < f; ++g) off += ef.k[g];
+    const Fr* rr = r + off;
+    const int a = k / 2, b = k - a;
+    const int nsc = (f == ef.nf - 1 && scale) ? 3 : 1;
+    const uint32_t t = threadIdx.x;
+    Fr one;
+    fe_one(one);
+    if (t < (1u << a) + (1u << b)) {
+        const bool isA = t < (1u << a);
+        const uint32_t i = isA ? t : t - (1u << a);
+        const int o = isA ? 0 : a, nb = isA ? a : b;
+        Fr acc = one;
+        for (int j = 0; j < nb; ++j) {
+            Fr rj = ld_fr(rr + o + j), fj;
+            if ((i >> j) & 1)
+                fj = rj;
+            else
+                fe_sub(fj, one, rj);
+            fe_mul(acc, acc, fj);
+        }
+        if (isA) {
+            A[i] = acc;
+        } else if (nsc == 1) {
+            B[i] = acc;
+        } else {
+            for (int m = 0; m < 3; ++m) {
+                Fr sm;
+                fe_mul(sm, acc, ld_fr(scale + m));
+                B[m * 128 + i] = sm;
+            }
+        }
     }
     __syncthreads();
-    // step j: tab[x + 2^j] = tab[x] * r_j, tab[x] *= (1 - r_j) for x < 2^j. Each thread touches
-    // only its own x and x + 2^j, so a barrier between steps is the only ordering needed.
-    for (int j = 0; j < k; ++j) {
-        const uint32_t half = 1u << j;
-        Fr rj = ld_fr(r + j), one, om;
-        fe_one(one);
-        fe_sub(om, one, rj);
-        for (uint32_t x = threadIdx.x; x < half; x += blockDim.x) {
-            Fr v = ld_fr(tab + x), a, b;
-            fe_mul(a, v, om);
-            fe_mul(b, v, rj);
-            st_fr(tab + x, a);
-            st_fr(tab + x + half, b);
+    const uint32_t cnt = 1u << k, amask = (1u << a) - 1;
+    Fr* dst = const_cast<Fr*>(ef.t[f]);
+    for (uint32_t x = t; x < cnt; x += blockDim.x) {
+        const Fr ax = A[x & amask];
+        for (int m = 0; m < nsc; ++m) {
+            Fr v;
+            fe_mul(v, ax, B[m * 128 + (x >> a)]);
+            st_fr(dst + (size_t)m * cnt + x, v);
         }
-        __syncthreads();
     }
 }
 
@@ -561,17 +610,8 @@ __global__ __launch_bounds__(kThreads) void k_sc2_fold_pair(const Fr* __restrict
 // lane then reads its own row. Only the wave itself touches its region, so there is no block
 // barrier: LDS operations of one wave complete in order, and `wave_lds_sync` keeps the compiler from
 // moving them across each other.
-#ifndef SPX_SC_WAVE_LDS
-#define SPX_SC_WAVE_LDS 1
-#endif
-#ifndef SPX_SC_WAVES4
-#define SPX_SC_WAVES4 1
-#endif
-#if SPX_SC_WAVES4  // 4 waves per SIMD (a few spilled registers) so a 2^20 round's 4096 waves fit one round
+// 4 waves per SIMD (a few spilled registers) so a 2^20 round's 4096 waves fit one round
 #define SPX_WAVE_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define SPX_WAVE_OCC
-#endif
 static constexpr int kWaveLdsChunks = 64 * 9;  // 16-byte chunks per wave: 64 rows of up to 8 + 1 pad
 DEV Fr shfl_fr(const Fr& a, int src) {
     Fr r;
@@ -1014,17 +1054,30 @@ void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* 
     }
 }
 
-void launch_col_stream(const ColStreamView& cv, const Fr* eq, Fr* out, const Fr* scale, const SparseView3& lv,
-                       const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows, Fr* partial,
-                       hipStream_t s) {
+EqFactors eq_factors_for(int L, Fr* scratch) {
+    EqFactors ef{};
+    if (L < 1 || L > 26) throw std::invalid_argument("eq_factors_for: 1..26 variables");
+    ef.nf = 2;  // lo (<= 2^13 entries) + 3 scaled copies of hi: <= kEqScratch entries, L2-resident
+    ef.k[0] = (L + 1) / 2;
+    ef.k[1] = L - ef.k[0];
+    ef.t[0] = scratch;
+    ef.t[1] = scratch + (1u << ef.k[0]);
+    return ef;
+}
+
+void launch_col_stream(const ColStreamView& cv, const Fr* r_x, int L, const Fr* scale, Fr* out, Fr* eq_scratch,
+                       const SparseView3& lv, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
+                       Fr* partial, hipStream_t s) {
+    const EqFactors ef = eq_factors_for(L, eq_scratch);
+    hipLaunchKernelGGL(k_eq_factors, dim3(ef.nf), dim3(kEqThreads), 0, s, r_x, ef, scale);
     if (cv.nslices) {
-        const uint32_t nwin = (cv.nslices + cv.spw - 1) / cv.spw;
-        hipLaunchKernelGGL(k_col_stream, dim3(nwin), dim3(kThreads), 0, s, cv, eq, out, scale);
+        const uint32_t nwin = (cv.nslices + kColWindow - 1) / kColWindow;
+        hipLaunchKernelGGL(k_col_stream, dim3(nwin), dim3(kThreads), 0, s, cv, ef, out);
     }
     if (nchunks > 0) {
-        hipLaunchKernelGGL(k_sparse_chunks, dim3(nchunks), dim3(kThreads), 0, s, lv, eq, chunks, partial);
-        hipLaunchKernelGGL(k_sparse_long_finish<1>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, out, nullptr,
-                           nullptr, scale);
+        hipLaunchKernelGGL(k_col_chunks, dim3(nchunks), dim3(kThreads), 0, s, lv, ef, chunks, partial);
+        hipLaunchKernelGGL(k_sparse_long_finish<0>, dim3(1), dim3(64), 0, s, lrows, nlrows, partial, out, out, out,
+                           nullptr);
     }
 }
 
@@ -1033,8 +1086,13 @@ void launch_eq_table(const Fr* r_dev, int k, uint64_t base, uint64_t count, Fr* 
     // split k = klo + khi, each <= 13 (k <= 26): the scratch halves hold 2^13 entries
     int klo = (k + 1) / 2, khi = k - klo;
     if (k < 0 || klo > 13) throw std::invalid_argument("launch_eq_table: more than 26 variables");
-    hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev, klo, scratch_lo);
-    hipLaunchKernelGGL(k_eq_small, dim3(1), dim3(kThreads), 0, s, r_dev + klo, khi, scratch_hi);
+    EqFactors ef{};
+    ef.nf = 2;
+    ef.k[0] = klo;
+    ef.k[1] = khi;
+    ef.t[0] = scratch_lo;
+    ef.t[1] = scratch_hi;
+    hipLaunchKernelGGL(k_eq_factors, dim3(2), dim3(kEqThreads), 0, s, r_dev, ef, nullptr);
     kp_begin(KP_EQ, s);
     hipLaunchKernelGGL(k_eq_expand, dim3(grid_for(count, 8192)), dim3(kThreads), 0, s, scratch_lo, scratch_hi, klo, base,
                        count, out);
@@ -1096,7 +1154,7 @@ void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr
                       uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC1, s);
-    if (SPX_SC_WAVE_LDS && half >= kWaveMinHalf) {
+    if (half >= kWaveMinHalf) {
         g = grid_for(half, kWaveMaxBlocks);
         if (fold && need1)
             sc1_wave_launch<true, true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
@@ -1106,7 +1164,7 @@ void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr
             sc1_wave_launch<false, true>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
         else
             sc1_wave_launch<false, false>(g, in, out, Ein, Eout, r, half, partial, ticket, result3, s);
-    } else if (SPX_SC_WAVE_LDS && fold && !need1) {  // small fold round: quad per pair, last-block reduction
+    } else if (fold && !need1) {  // small fold round: quad per pair, last-block reduction
         g = grid_for(4 * half, kFuseMaxBlocks);
         hipLaunchKernelGGL(k_sc1_fold_quad<true>, dim3(g), dim3(kThreads), 0, s, in, out, Ein, Eout, r, half, partial,
                            ticket, result3);
@@ -1123,7 +1181,7 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
                       Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s) {
     int g = sc_grid(half);
     kp_begin(KP_SC2, s);
-    if (SPX_SC_WAVE_LDS && half >= kWaveMinHalf) {
+    if (half >= kWaveMinHalf) {
         g = grid_for(half, kWaveMaxBlocks);
         if (fold && need1)
             sc2_wave_launch<true, true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
@@ -1133,7 +1191,7 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
             sc2_wave_launch<false, true>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
         else
             sc2_wave_launch<false, false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, s);
-    } else if (SPX_SC_WAVE_LDS && fold && !need1) {  // small fold round: lane pair per pair
+    } else if (fold && !need1) {  // small fold round: lane pair per pair
         g = grid_for(2 * half, kFuseMaxBlocks);
         hipLaunchKernelGGL(k_sc2_fold_pair<true>, dim3(g), dim3(kThreads), 0, s, Min, Zin, Mout, Zout, r, half, partial,
                            ticket, result3);
@@ -1167,7 +1225,7 @@ void launch_open_fold(const Fr* rin, Fr* rout, Fr* q, int nf, const Fr* points, 
     const int g = grid_for(nout, 8192);
     double qw = 0;
     for (int j = 0; j < nf; ++j) qw += qoffs[j] != ~0ull ? (double)(nout << (nf - 1 - j)) : 0.0;
-    const bool wave = SPX_SC_WAVE_LDS && nout >= kWaveMinHalf;  // whole waves of 64 outputs
+    const bool wave = nout >= kWaveMinHalf;  // whole waves of 64 outputs
     if (nf == 3) {
         FoldArgs<3> a;
         for (int j = 0; j < 3; ++j) a.p[j] = points[j], a.qoff[j] = qoffs[j];

@@ -71,7 +71,7 @@ template <bool COMPACT>
 __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
                                                      int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t cap,
-                                                     uint32_t* __restrict__ st, uint32_t* __restrict__ hist) {
+                                                     uint32_t* __restrict__ st) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = g < total;
     if (!COMPACT && !live) return;
@@ -95,7 +95,6 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
             const uint64_t o = I.ref_off + (uint64_t)w * I.size + j;
             keys[o] = key == ~0u ? nb : key;
             vals[o] = digit_ref(I, w, j, d);
-            if (hist && key != ~0u) atomicAdd(&hist[key], 1u);
         }
     } else {
         // the digits are extracted once: for up to kKeep windows (c >= 16 at the sizes that matter) the
@@ -138,7 +137,6 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                     if (pos < cap) {
                         keys[pos] = kkey[w];
                         vals[pos] = kref[w];
-                        if (hist) atomicAdd(&hist[kkey[w]], 1u);
                     }
                     ++pos;
                 }
@@ -152,7 +150,6 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                 if (pos < cap) {
                     keys[pos] = key;
                     vals[pos] = digit_ref(I, w, j, dg);
-                    if (hist) atomicAdd(&hist[key], 1u);
                 }
                 ++pos;
             }
@@ -182,18 +179,6 @@ __global__ __launch_bounds__(kLight) void k_bucket_bounds(const uint32_t* __rest
             hi = mid;
     }
     offs[b] = (uint32_t)lo;
-}
-
-// Counting sort's scatter: bucket b's references go to [offs[b], offs[b] + cnt[b]) in any order (group
-// addition is exact and commutative), each slot taken by decrementing the bucket's count.
-__global__ __launch_bounds__(kLight) void k_bucket_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                           uint64_t n, uint32_t nb, const uint32_t* __restrict__ offs,
-                                                           uint32_t* __restrict__ cnt, uint32_t* __restrict__ refs) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = keys[i];
-    if (k >= nb) return;
-    refs[offs[k] + atomicSub(&cnt[k], 1u) - 1u] = vals[i];
 }
 
 // Exclusive offsets of a per-bucket count derived from the previous offsets (device-wide hipCUB
@@ -230,34 +215,20 @@ void scan_segs(MsmWorkspace* ws, const uint32_t* off, uint32_t nb, uint32_t seg,
     scan_op(ws, SegsOp{off, nb, seg}, nb, seg_off, s);
 }
 
-uint32_t seg1_len(bool g2) {
-    static const uint32_t v1 = [] {
-        const char* e = getenv("SPX_KSEG1");
-        return e ? (uint32_t)std::max(1, atoi(e)) : kSeg1Default;
-    }();
-    static const uint32_t v2 = [] {
-        const char* e = getenv("SPX_KSEG1_G2");
-        return e ? (uint32_t)std::max(1, atoi(e)) : v1;
-    }();
-    return g2 ? v2 : v1;
-}
+uint32_t seg1_len(bool) { return kSeg1Default; }
 
 // The accumulation kernel's threads all run the same number of additions, so its duration is
 // (rounds of resident waves) x (one wave's chain of seg1 additions). A grid of 4.02 rounds takes as
 // long as 5: seg1 is lowered to the smallest value that keeps the round count, so the last round is
-// full. SPX_SEG1_FIT=0 keeps the fixed length (tuning).
+// full (the fixed length measured 1.5% slower: profiles/r02_ab8_seg1fit.jsonl, r02_ab20_seg.jsonl).
 uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem) {
-    static const int on = [] {
-        const char* e = getenv("SPX_SEG1_FIT");
-        return e ? atoi(e) : 1;
-    }();
     static const int cus = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             n = 0;
         return n;
     }();
-    if (!on || cus <= 0 || refs == 0) return seg1;
+    if (cus <= 0 || refs == 0) return seg1;
     const uint64_t slots = (uint64_t)cus * 4 * waves_per_simd * 64 / lanes_per_elem;  // resident elements
     const uint64_t nthr = (refs + seg1 - 1) / seg1;
     const uint64_t rounds = (nthr + slots - 1) / slots;
@@ -387,20 +358,6 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
     p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
 }
 
-#ifndef SPX_SORT_BITS
-#define SPX_SORT_BITS 0  // A/B knob: 11-bit rocPRIM onesweep digits measured no faster (profiles/r03/r03at_ab_sort_bits.jsonl)
-#endif
-#ifndef SPX_SORT_MERGE_LIMIT  // below this many keys rocPRIM sorts by merging (its default: 2^20)
-#define SPX_SORT_MERGE_LIMIT (1024 * 1024)
-#endif
-#if SPX_SORT_BITS
-using SortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, SPX_SORT_BITS,
-                                        rocprim::block_radix_rank_algorithm::match>,
-    SPX_SORT_MERGE_LIMIT>;
-#endif
-
 MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s) {
     MsmSorted o;
     const uint32_t nb = p.nb;
@@ -415,44 +372,16 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * std::max<uint64_t>(n, 1));
     uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
     const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
-    // SPX_MSM_SORT=count: counting sort (histogram atomics in the keys pass, scan, scatter), no
-    // decoupled look-back; default: hipCUB's radix sort (onesweep)
-    static const bool count_sort = [] {
-        const char* e = getenv("SPX_MSM_SORT");
-        return e && std::string(e) == "count";
-    }();
-    uint32_t* hist = nullptr;
-    if (count_sort) {
-        hist = (uint32_t*)ws->hist.ensure(4 * (nb + 1));
-        HIPCHK(hipMemsetAsync(hist, 0, 4 * (nb + 1), s));
-    }
+    // (a counting sort, histogram atomics in the keys pass + scan + scatter, measured 10% slower end to
+    // end: profiles/r03/r03t_ab.jsonl; 11-bit onesweep digits no faster: r03at_ab_sort_bits.jsonl)
     kp_begin(KP_SORT, s);
     if (p.compact)
         hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, (uint32_t)n, st, hist);
+                           scalars, ka, va, (uint32_t)n, st);
     else
         hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, 0u, st, hist);
-    if (count_sort) {
-        size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hist, o.offs, (int)nb + 1, s));
-        void* t = ws->cub.ensure(tb);
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, hist, o.offs, (int)nb + 1, s));
-        hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, ka, va, n, nb,
-                           o.offs, hist, o.refs);
-    } else {
-#if SPX_SORT_BITS
-        // rocPRIM onesweep with SPX_SORT_BITS-bit digits (the gfx950 default is 8): the bucket keys of an
-        // opening batch span 17-20 bits (2^15 / G buckets x ~20 instances), so 2 passes instead of 3.
-        // Measured: the sort's time per proof is unchanged at N = 1 and G = 8 is 2% slower, so it is off.
-        rocprim::double_buffer<uint32_t> dk(ka, kb), dv(va, o.refs);
-        size_t tb = 0;
-        HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, dk, dv, n, 0u, (unsigned)bits, s));
-        void* t = ws->cub.ensure(tb);
-        HIPCHK(rocprim::radix_sort_pairs<SortCfg>(t, tb, dk, dv, n, 0u, (unsigned)bits, s));
-        o.refs = dv.current();
-        const uint32_t* sorted = dk.current();
-#else
+                           scalars, ka, va, 0u, st);
+    {
         hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
         size_t tb = 0;
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
@@ -460,7 +389,6 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
         o.refs = dv.Current();
         const uint32_t* sorted = dk.Current();
-#endif
         hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, sorted, n, nb,
                            o.offs);
     }

@@ -13,17 +13,11 @@
 namespace spx {
 
 static constexpr uint32_t kSeg1Default = 64;  // references per thread, affine accumulation level (A/B: profiles/r02_ab19_seg.jsonl, r02_ab20_seg.jsonl)
-uint32_t seg1_len(bool g2);                      // kSeg1Default unless SPX_KSEG1 / SPX_KSEG1_G2 (tuning)
+uint32_t seg1_len(bool g2);                      // kSeg1Default for both curves
 // seg1 lowered so the accumulation grid fills whole rounds of resident waves (no near-empty last round)
 uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem);
-#ifndef SPX_XYZZ_SEG
-#define SPX_XYZZ_SEG 4
-#endif
-static constexpr uint32_t kSeg = SPX_XYZZ_SEG;  // partials per thread, XYZZ accumulation levels (4: shallow levels)
-#ifndef SPX_TREE_CHUNK_LOG
-#define SPX_TREE_CHUNK_LOG 2
-#endif
-static constexpr uint32_t kTreeChunkLog = SPX_TREE_CHUNK_LOG;  // buckets per running-sum chunk of the weighting leaf: 4
+static constexpr uint32_t kSeg = 4;           // partials per thread, XYZZ accumulation levels (4: shallow levels)
+static constexpr uint32_t kTreeChunkLog = 2;  // buckets per running-sum chunk of the weighting leaf: 4
 static constexpr uint32_t kTopNodes = 16;  // k_tree_top: the levels whose input has <= 16 nodes, one launch
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
@@ -113,7 +107,7 @@ struct PinArena {
 };
 
 struct MsmWorkspace {
-    DBuf tables, offs, refs, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a, hist;
+    DBuf tables, offs, refs, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a;
     // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
     // rank's buckets (e.g. many equal values) stops overflowing after its first batch
     double cap_scale = 1.0;

@@ -1,9 +1,4 @@
 // G1 instantiation of the MSM / PP-preprocessing / keygen kernels (see msm_impl.hpp).
-// independent 64-bit accumulation chains per Montgomery column (ff29.hpp)
-#ifndef SPX_G1_CHAINS
-#define SPX_G1_CHAINS 1
-#endif
-#define SPX_F29_CHAINS SPX_G1_CHAINS
 #include "msm_impl.hpp"
 
 namespace spx {

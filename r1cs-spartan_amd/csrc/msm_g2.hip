@@ -1,10 +1,4 @@
 // G2 instantiation of the MSM / PP-preprocessing / keygen kernels (see msm_impl.hpp).
-// independent 64-bit accumulation chains per Montgomery column (ff29.hpp); 1: two chains measured
-// 4% slower (profiles/r02_ab7_chains.jsonl, r02_ubench_madd.txt), three spill
-#ifndef SPX_G2_CHAINS
-#define SPX_G2_CHAINS 1
-#endif
-#define SPX_F29_CHAINS SPX_G2_CHAINS
 #include "msm_impl.hpp"
 
 namespace spx {

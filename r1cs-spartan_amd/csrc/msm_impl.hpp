@@ -12,15 +12,6 @@ namespace spx {
 // so a G2 lane holds half a point and two waves fit each SIMD.
 template <class F>
 struct Acc;
-#ifndef SPX_G1_WAVES
-#define SPX_G1_WAVES 1
-#endif
-#ifndef SPX_G2_WAVES
-#define SPX_G2_WAVES 2
-#endif
-#ifndef SPX_ACC_PREFETCH
-#define SPX_ACC_PREFETCH 0
-#endif
 // one lane's packed affine coordinates (G1: the point; G2: its half), as loaded from the table
 struct AffRaw {
     Fq x, y;
@@ -30,7 +21,7 @@ struct Acc<Fq> {
     using Pt = G1Slot;  // window-table element: one 128-byte line per point
     using T = F29;
     using TA = F29;  // the accumulation kernel's element type
-    static constexpr int kLanes = 1, kWaves = SPX_G1_WAVES;
+    static constexpr int kLanes = 1, kWaves = 1;
     static DEV void ld_raw(AffRaw& a, const G1Slot* p) { load_vec(*(Aff<Fq>*)&a, &p->p); }
     static DEV void unpack(T& x, T& y, const AffRaw& a) {
         f29_unpack(x, a.x.v);
@@ -48,16 +39,11 @@ struct Acc<Fq> {
 template <>
 struct Acc<Fq2> {
     using Pt = Aff<Fq2>;  // 192 bytes: 1.5 lines, the lane pair's halves 96 bytes each
-#ifndef SPX_G2_WEIGHT_BORROW_FREE
-#define SPX_G2_WEIGHT_BORROW_FREE 0
-#endif
-#if SPX_G2_WEIGHT_BORROW_FREE
-    using T = FP29A;
-#else
+    // borrow-free operand preparation in the accumulation only (fq2pair.hpp); the weighting kernels,
+    // at 256 registers already, keep the borrow-chain form (the borrow-free one spilled there)
     using T = FP29;
-#endif
-    using TA = FP29A;  // borrow-free operand preparation in the accumulation only (fq2pair.hpp)
-    static constexpr int kLanes = 2, kWaves = SPX_G2_WAVES;
+    using TA = FP29A;
+    static constexpr int kLanes = 2, kWaves = 2;
     static DEV void ld_raw(AffRaw& a, const Aff<Fq2>* p) {
         const bool odd = pair_odd();
         load_vec(a.x, odd ? &p->x.c1 : &p->x.c0);
@@ -221,36 +207,19 @@ DEV void x29_add_split(X29<T>& p, const X29<T>& q) {
     p.zzz = S2::sel(h, z4o, z4);
 }
 
-#ifndef SPX_G2_QUAD
-#define SPX_G2_QUAD 1
-#endif
-#ifndef SPX_G1_SPLIT
-#define SPX_G1_SPLIT 1
-#endif
-// lanes per element in the weighting / partial kernels: G2 a quad, G1 a pair (split additions)
+// lanes per element in the weighting / partial kernels: G2 a quad, G1 a pair (split additions: the
+// two halves of an element take different products of one addition)
 template <class F>
-struct TreeLanes;
-template <>
-struct TreeLanes<Fq> {
-    static constexpr int v = SPX_G1_SPLIT ? 2 : 1;
-};
-template <>
-struct TreeLanes<Fq2> {
-    static constexpr int v = SPX_G2_QUAD ? 4 : 2;
+struct TreeLanes {
+    static constexpr int v = 2 * Acc<F>::kLanes;
 };
 template <class F>
 DEV void tree_add(X29<typename Acc<F>::T>& p, const X29<typename Acc<F>::T>& q) {
-    if constexpr (TreeLanes<F>::v == 2 * Acc<F>::kLanes)
-        x29_add_split(p, q);
-    else
-        x29_add(p, q);
+    x29_add_split(p, q);
 }
 template <class F>
 DEV void tree_dbl(X29<typename Acc<F>::T>& p) {
-    if constexpr (TreeLanes<F>::v == 2 * Acc<F>::kLanes)
-        x29_dbl_split(p);
-    else
-        x29_dbl(p);
+    x29_dbl_split(p);
 }
 template <class F>
 DEV uint64_t tree_elem() {
@@ -296,11 +265,6 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
     uint32_t slot = pfx[b] + (t - off[b] / seg1);
     X29<T> acc;
     x29_set_inf(acc);
-#if SPX_ACC_PREFETCH
-    uint32_t rn = refs[e];
-    AffRaw nxt;
-    A::ld_raw(nxt, pts + (rn & 0x7fffffffu));
-#endif
     for (; e < end; ++e) {
         if (e == bend) {  // bucket b is finished inside this range: the next one starts here
             A::st(out + slot, acc);
@@ -311,23 +275,10 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_accum_aff(const uint
             bend = off[b + 1];
             slot = pfx[b];
         }
-        // (a software-pipelined variant that issues the next point's load before this addition
-        // measured 2.5% slower end to end: more AGPR traffic at occupancy 1)
-#if SPX_ACC_PREFETCH
-        // the next reference's point is loaded before this addition (its latency hides behind it)
-        const uint32_t r = rn;
-        const AffRaw cur = nxt;
-        if (e + 1 < end) {
-            rn = refs[e + 1];
-            A::ld_raw(nxt, pts + (rn & 0x7fffffffu));
-        }
-        T px, py;
-        A::unpack(px, py, cur);
-#else
+        // (issuing the next point's load before this addition measured within noise: DESIGN.md 4.1)
         const uint32_t r = refs[e];
         T px, py;
         A::ld_aff(px, py, pts + (r & 0x7fffffffu));
-#endif
         if (A::aff_sentinel(px, py)) continue;
         x29_madd(acc, px, py, (r >> 31) != 0);
     }

@@ -69,23 +69,11 @@ uint8_t* Ctx::pin_at(size_t off, size_t bytes, size_t region) {
 
 
 // ====================================================================== public parameters
+// Pippenger window bits: 16 for >= 2^14 points (wider windows for >= 2^18 and narrower ones for
+// 2^14-2^17 measured slower or equal: profiles/r02_ab6_window_bits.jsonl, r02_ab7_window_mid.jsonl)
 int window_bits_for(uint64_t size) {
-    // SPX_WINDOW_BITS_LARGE (tuning): window bits for MSMs of >= 2^18 points (default 16)
-    static const int large = [] {
-        const char* e = getenv("SPX_WINDOW_BITS_LARGE");
-        const int v = e ? atoi(e) : 16;
-        return (v >= 12 && v <= 22) ? v : 16;
-    }();
-    // SPX_WINDOW_MID (tuning): for 2^14..2^17 points, c = min(16, log2(size) - MID) (0: 16)
-    static const int mid = [] {
-        const char* e = getenv("SPX_WINDOW_MID");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 0 && v <= 6) ? v : 0;
-    }();
-    int k = size ? ilog2(size) : 0;
-    if (k >= 18) return large;
-    if (k >= 14) return mid ? std::min(16, k - mid) : 16;
-    return std::max(3, k - 2);
+    const int k = size ? ilog2(size) : 0;
+    return k >= 14 ? 16 : std::max(3, k - 2);
 }
 static int windows_for(int c) { return (256 + c - 1) / c; }
 
@@ -451,7 +439,7 @@ static void build_csc(const HostCsr& M, uint64_t n, std::vector<uint64_t>& cp, s
 
 // The column stream of the rank-local columns [lo, lo + cnt) of (up to) three CSC matrices for
 // k_col_stream (kernels.hpp: ColStreamView). A column's entries are A's, then B's, then C's (rows
-// ascending); columns are sorted by entry count, longest first, inside windows of 64 spw columns and
+// ascending); columns are sorted by entry count, longest first, inside windows of 64 kColWindow columns and
 // dealt to the lanes of 64-column slices, so a wave's lanes run columns of nearly equal length (the
 // per-column loop left lanes of Poisson-length columns idle for most of a wave's steps). Columns with
 // more than kLongCol entries take the chunked long path instead.
@@ -468,11 +456,7 @@ static void upload_cols(Ctx& C, DevColStream& D, const std::vector<uint64_t>* cp
         if (L > kLongCol) long_cols.push_back(y);
     }
     D.entries = live;
-    // one block (4 waves) per window: the widest window (<= 16 slices) that still gives >= 512 blocks
-    uint32_t spw = 16;
-    while (spw > 4 && (cnt + 64 * spw - 1) / (64 * spw) < 512) spw >>= 1;
-    D.spw = spw;
-    const uint64_t win = 64ull * spw, nslices = (cnt + 63) / 64;
+    const uint64_t win = 64ull * kColWindow, nslices = (cnt + 63) / 64;
     D.nslices = (uint32_t)nslices;
     std::vector<ColSlice> sl(nslices);
     std::vector<uint32_t> lanes(64 * nslices, kColNone);
@@ -572,7 +556,9 @@ static void upload_cols(Ctx& C, DevColStream& D, const std::vector<uint64_t>* cp
     C.sync();
 }
 
-static void feed_matrix(Blake2s& h, const HostCsr& m) {
+// sink: update(data, len) of one state or of a group of states absorbing the same bytes
+template <class Sink>
+static void feed_matrix(Sink&& h, const HostCsr& m) {
     // CanonicalSerialize of MatrixExtension { constraint: Vec<Vec<(F, usize)>>, num_constraints: usize },
     // streamed through a 64 KiB staging block (u64 lengths, then (32-byte Fr, u64 column) per entry)
     constexpr size_t kBlk = 1 << 16;
@@ -604,6 +590,16 @@ Blake2s absorb_matrices(const Index& I) {
     Blake2s h;
     for (int m = 0; m < 3; ++m) feed_matrix(h, I.m[m]);
     return h;
+}
+
+void absorb_matrices_lanes(const Index& I, Blake2s* out, int k) {
+    for (int l = 0; l < k; ++l) out[l].reset();
+    struct Lanes {
+        Blake2s* st;
+        int k;
+        void update(const void* d, size_t n) { blake2s_update_lanes(st, k, d, n); }
+    } sink{out, k};
+    for (int m = 0; m < 3; ++m) feed_matrix(sink, I.m[m]);
 }
 
 std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
@@ -643,9 +639,9 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
         double e_rows = 0;
         for (int m = 0; m < 3; ++m) e_rows += (double)(mats[m].rp[lo + nl] - mats[m].rp[lo]);
         I->rows_bytes = 68.0 * e_rows + 3.0 * 8.0 * nl + 3.0 * 32.0 * nl;  // 3 outputs
-        // column stream: 32 B value + 4 B row|matrix + 32 B gathered eq per entry; 4 B lane word and
-        // one combined 32 B output per column
-        I->cols_bytes = 68.0 * (double)I->cols.entries + 4.0 * nl + 32.0 * nl;
+        // column stream: 32 B value + 4 B row|matrix per entry (eq(r_x) is gathered from its two
+        // cache-resident factor tables, not from HBM); 4 B lane word and one 32 B output per column
+        I->cols_bytes = 36.0 * (double)I->cols.entries + 4.0 * nl + 32.0 * nl;
     }
     int herr = 0;
     SPX_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, C.stream));
@@ -1071,11 +1067,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     const uint64_t need = 3 * nl        // Az Bz Cz
                           + 3 * n2 + 3 * n4  // fold ping-pong
                           + n2 + n4 + std::max<uint64_t>(nl / 8, 1)  // E tables
-                          + n                // eq(r_x)
                           + nl + n2 + n4     // Mrx + fold
                           + n2 + n4          // z fold
                           + std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks))
-                          + 8192 * 2 + 64 + 8 * L;  // partials, eq scratch, challenges
+                          + 8192 * 2 + kEqScratch + 64 + 8 * L;  // partials, eq scratch, challenges
     C.scratch.ensure(32 * need);
     Fr* base = C.scratch.as<Fr>();
     uint64_t cur_off = 0;
@@ -1088,11 +1083,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Fr* F1[3] = {take(n2), take(n2), take(n2)};
     Fr* F2[3] = {take(n4), take(n4), take(n4)};
     Fr *E1 = take(n2), *Ea = take(n4), *Eb = take(std::max<uint64_t>(nl / 8, 1));
-    Fr* EQ = take(n);
     Fr *M0 = take(nl), *M1 = take(n2), *M2 = take(n4);
     Fr *Z1 = take(n2), *Z2 = take(n4);
     Fr* partial = take(std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks)));
-    Fr *eqlo = take(8192), *eqhi = take(8192);
+    Fr *eqlo = take(8192), *eqhi = take(8192), *eqf = take(kEqScratch);
     Fr* chdev = take(8 * L);  // tau, r_x, (r_a, r_b, r_c), ...
     uint8_t* hp = C.pin_at(Ctx::kPinHp, 1 << 16, 64 << 10);
 
@@ -1331,10 +1325,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     memcpy(hp, r_x.data(), 32 * L);
     memcpy(hp + 32 * L, rabc, 96);
     SPX_HIP(hipMemcpyAsync(rxdev, hp, 32 * (L + 3), hipMemcpyHostToDevice, C.stream));
-    launch_eq_table(rxdev, L, 0, n, EQ, eqlo, eqhi, C.stream);
     {
         kp_begin(KP_MTV, C.stream);
-        I.cols.launch(EQ, M0, rxdev + L, partial, C.stream);
+        I.cols.launch(rxdev, L, rxdev + L, M0, eqf, partial, C.stream);
         kp_end(I.cols_bytes, C.stream);
     }
     {
@@ -1613,18 +1606,17 @@ static HFr eval_matrices_at(Ctx& C, Index& I, const std::vector<HFr>& r_x, const
     const int L = I.log_n;
     const uint64_t n = I.n;
     const uint64_t parts = std::max<uint64_t>(3 * 2048, (uint64_t)I.cols.longc.nchunks);
-    C.scratch.ensure(32 * (n + n + n / 2 + 2 + parts + 8192 * 2 + 4 * L + 8));
+    C.scratch.ensure(32 * (n + n + n / 2 + 2 + parts + kEqScratch + 4 * L + 8));
     Fr* base = C.scratch.as<Fr>();
-    Fr *EQ = base, *M0 = EQ + n, *Mb = M0 + n, *partial = Mb + n / 2 + 2, *eqlo = partial + parts, *eqhi = eqlo + 8192;
-    Fr* ch = eqhi + 8192;  // r_x (L), r_abc (3), r_y (L)
+    Fr *EQ = base, *M0 = EQ + n, *Mb = M0 + n, *partial = Mb + n / 2 + 2, *eqf = partial + parts;
+    Fr* ch = eqf + kEqScratch;  // r_x (L), r_abc (3), r_y (L)
     std::vector<HFr> hch(r_x);
     hch.insert(hch.end(), rabc, rabc + 3);
     hch.insert(hch.end(), r_y.begin(), r_y.end());
     uint8_t* hs = C.pin_at(Ctx::kPinStage, 32 * hch.size(), 64 << 10);
     memcpy(hs, hch.data(), 32 * hch.size());
     SPX_HIP(hipMemcpyAsync(ch, hs, 32 * hch.size(), hipMemcpyHostToDevice, C.stream));
-    launch_eq_table(ch, L, 0, n, EQ, eqlo, eqhi, C.stream);
-    I.cols.launch(EQ, M0, ch + L, partial, C.stream);
+    I.cols.launch(ch, L, ch + L, M0, eqf, partial, C.stream);
     // fold at r_y (variable 0 = LSB): M0 -> EQ (as q scratch) / Mb ping-pong
     const Fr* rin = M0;
     Fr* bufs[2] = {Mb, M0};
@@ -1772,8 +1764,7 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     std::vector<uint32_t> cols[3] = {rows, {}, {}};
     std::vector<uint8_t> vv[3] = {vals, {}, {}};
     DevColStream D;
-    DevMem err(sizeof(int)), rx(32 * L + 96), eq(32 * n), out(32 * n * 2), part(32 * std::max(4096, 1)), lo(32 << 14),
-        hi(32 << 14);
+    DevMem err(sizeof(int)), rx(32 * L + 96), out(32 * n * 2), part(32 * std::max(4096, 1)), eqf(32 * kEqScratch);
     SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
     upload_cols(C, D, rps, cols, vv, 0, n, err.as<int>());
     std::vector<uint8_t> hr(32 * L + 96, 0);
@@ -1784,10 +1775,9 @@ std::vector<uint8_t> k_eval_on_x(Ctx& C, const HostCsr& m, const uint8_t* r_x) {
     memcpy(hr.data() + 32 * L, onec, 32);  // canonical 1, 0, 0
     SPX_HIP(hipMemcpyAsync(rx.p, hr.data(), hr.size(), hipMemcpyHostToDevice, C.stream));
     launch_to_mont(rx.as<Fr>(), L + 3, err.as<int>(), C.stream);
-    launch_eq_table(rx.as<Fr>(), L, 0, n, eq.as<Fr>(), lo.as<Fr>(), hi.as<Fr>(), C.stream);
     if (D.longc.nchunks > 4096) part.alloc(32 * D.longc.nchunks);
     Fr* o = out.as<Fr>();
-    D.launch(eq.as<Fr>(), o, rx.as<Fr>() + L, part.as<Fr>(), C.stream);
+    D.launch(rx.as<Fr>(), L, rx.as<Fr>() + L, o, eqf.as<Fr>(), part.as<Fr>(), C.stream);
     launch_from_mont(o + n, o, n, C.stream);
     std::vector<uint8_t> res(32 * n);
     SPX_HIP(hipMemcpyAsync(res.data(), o + n, 32 * n, hipMemcpyDeviceToHost, C.stream));
@@ -1807,7 +1797,7 @@ void k_sumcheck_round(Ctx& C, const uint8_t* f, const uint8_t* g, uint64_t n, co
     if (!is_pow2(n) || n < (r_prev ? 4u : 2u)) invalid("table size must be a power of two (>= 2, >= 4 with a challenge)");
     const bool fold = r_prev != nullptr;
     const uint64_t half = fold ? n / 4 : n / 2;
-    DevMem err(sizeof(int)), tabs(32 * 2 * n), outs(32 * (fold ? n : 2)), res(32 * 3 + 32 * n),
+    DevMem err(sizeof(int)), tabs(32 * 2 * n), outs(32 * (fold ? n : 2)), res(32 * (3 + std::max<uint64_t>(n, 3))),
         part(32 * kRoundPartials);
     SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
     Fr* F = tabs.as<Fr>();

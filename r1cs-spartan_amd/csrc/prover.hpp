@@ -251,15 +251,16 @@ struct DevSparse {  // rank-local block of 3 matrices (CSR rows or CSC columns)
 };
 struct DevColStream {  // rank-local columns of A, B, C for eval_on_x (kernels.hpp: ColStreamView)
     DevMem slices, lanes, rowm, val;
-    uint32_t nslices = 0, spw = 4;
+    uint32_t nslices = 0;
     DevSparse longc;  // columns of more than kLongCol entries: per-matrix entry arrays + chunks
     uint64_t entries = 0;  // live entries (algorithmic bytes)
     ColStreamView view() const {
-        return ColStreamView{slices.as<ColSlice>(), lanes.as<uint32_t>(), rowm.as<uint32_t>(), val.as<Fr>(), nslices, spw};
+        return ColStreamView{slices.as<ColSlice>(), lanes.as<uint32_t>(), rowm.as<uint32_t>(), val.as<Fr>(), nslices};
     }
-    void launch(const Fr* eq, Fr* out, const Fr* scale, Fr* partial, hipStream_t s) const {
-        launch_col_stream(view(), eq, out, scale, longc.view(), longc.chunks.as<LongChunk>(), longc.nchunks,
-                          longc.lrows.as<LongRow>(), longc.nlrows, partial, s);
+    // out = sum_m scale[m] M(r_x, .) (eq_scratch: kEqScratch Fr)
+    void launch(const Fr* r_x, int L, const Fr* scale, Fr* out, Fr* eq_scratch, Fr* partial, hipStream_t s) const {
+        launch_col_stream(view(), r_x, L, scale, out, eq_scratch, longc.view(), longc.chunks.as<LongChunk>(),
+                          longc.nchunks, longc.lrows.as<LongRow>(), longc.nlrows, partial, s);
     }
 };
 struct Index {
@@ -297,6 +298,8 @@ struct ProveOpts {
 };
 // Blake2s state after absorbing A, B, C (lib.rs:61-64): the per-proof sequential host work
 Blake2s absorb_matrices(const Index& I);
+// the same absorption for k proofs at once (multi-buffer BLAKE2s: k equal states in vector lanes)
+void absorb_matrices_lanes(const Index& I, Blake2s* out, int k);
 
 // entry points used by the C ABI
 std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len);

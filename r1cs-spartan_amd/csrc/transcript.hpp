@@ -112,11 +112,18 @@ class Blake2s {
         for (int i = 0; i < 8; ++i) h_[i] ^= v[i] ^ v[i + 8];
     }
    private:
+    friend struct Blake2sLanes;
     uint32_t h_[8];
     uint32_t t0_, t1_;
     uint8_t buf_[64];
     size_t buflen_;
 };
+
+// Multi-buffer update (blake2s_lanes.cpp): st[0..k) absorb the same bytes; states at the same
+// position (counter, buffered bytes) advance together in the lanes of one vector (16 with AVX-512,
+// 8 with AVX2), others one by one. Results equal k separate update() calls.
+int blake2s_lane_width();
+void blake2s_update_lanes(Blake2s* st, int k, const void* data, size_t len);
 
 // The verifier of an interactive prove (the reference's round-level API, prover.rs:109-281 driven as
 // in ahp/tests.rs:8-70): every prover message goes to message(), every challenge comes from draw()

@@ -74,8 +74,8 @@ def _drive(spx, pk, inst, pp, seed, log_n, log_v):
 @pytest.mark.parametrize("kind,log_n,log_v,param", [(1, 8, 2, 1), (0, 6, 3, 0), (3, 10, 4, 0)])
 def test_interactive_rounds_match_oracle(spx, ctx, oc, kind, log_n, log_v, param):
     inst = oc.Instance(kind, log_n, log_v, 0x5EED0000 + log_n, param)
-    ppc = oc.PP.keygen(log_n, 77 + log_n)
-    pp = spx.PublicParameter.load(ctx, ppc.serialize())
+    pp = spx.MLProofForR1CS.setup(ctx, log_n, 77 + log_n)  # GPU keygen: its VerifierParameter is known
+    ppc = oc.PP.load(pp.serialize_uncompressed())
     pk = spx.MLArgumentForR1CS.index(ctx, *[spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats])
     seed = 99 + log_n
     msgs, pm6 = _drive(spx, pk, inst, pp, seed, log_n, log_v)

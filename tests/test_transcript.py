@@ -33,3 +33,18 @@ def test_sumcheck1_message_stepping(tmp_path):
                            os.path.join(ROOT, "tests", "native", "sc_message_check.cpp"), "-o", exe])
     out = subprocess.check_output([exe], timeout=120).decode()
     assert out.startswith("ok"), out
+
+
+def test_blake2s_lanes_match_scalar(tmp_path):
+    """blake2s_lanes.cpp (multi-buffer absorption of several proofs' matrices): every lane equals a
+    scalar stream over the same pieces, for lane counts below / at / above the vector width"""
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if not cxx:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path / "b2lanes")
+    csrc = os.path.join(ROOT, "r1cs-spartan_amd", "csrc")
+    subprocess.check_call([cxx, "-O3", "-std=c++17", "-w", "-I", csrc, os.path.join(csrc, "blake2s_lanes.cpp"),
+                           os.path.join(ROOT, "tests", "native", "blake2s_lanes_check.cpp"), "-o", exe])
+    out = subprocess.check_output([exe], timeout=300).decode()
+    assert out.startswith("ok"), out
+    print(out)

@@ -2,10 +2,13 @@
 //   k_madd: x29_madd (madd-2008-s, lane-pair Fq2) in a loop — the hot loop of k_accum_aff<Fq2>,
 //           ~100 KB of straight-line code per iteration;
 //   k_mul : the lane-pair Fq2 product alone, 10 per iteration in a non-unrolled loop (~5 KB of code).
-// Built once per SPX_F29_CHAINS value (-DSPX_F29_CHAINS=N). The per-product cost of k_madd over
+// (Round 2 built this once per SPX_F29_CHAINS value; the chain variant was dropped: one chain.) The per-product cost of k_madd over
 // that of k_mul separates the formula's own overhead (additions, selects, instruction supply) from
 // the product's issue cost. Operands are random field-sized values, not curve points: the formula's
 // cost does not depend on them (no exceptional branch is taken).
+#ifndef SPX_F29_CHAINS
+#define SPX_F29_CHAINS 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

@@ -513,6 +513,8 @@ def main():
                     "per rank shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm). "
                     "The other transport is measured beside it (value_comm_<other>) unless --one-comm")
     ap.add_argument("--one-comm", action="store_true", help="N > 1: measure the headline transport only")
+    ap.add_argument("--comm-deadline", type=float, default=300.0,
+                    help="N > 1: seconds the second transport's measurement may take before the line is printed without it")
     ap.add_argument("--launch-only", action="store_true",
                     help="start the ranks and report RANK / WORLD_SIZE without any HIP call (launcher test)")
     ap.add_argument("--inflight", type=int, default=0,
@@ -682,22 +684,6 @@ def main():
             p4, el1 = timed(single_fn(octxs[0], opk))
             assert p4 == ref[0], "proof-sharded single proof differs"
         other = [el, el1]
-    # ---- N > 1: the same proof-sharded pipeline on the other transport (shm <-> RCCL over xGMI), so one
-    # run reports both. The contexts, index and witnesses stay; only their communicator changes.
-    xcomm = None
-    if sctxs and not args.one_comm:
-        alt = "rccl" if args.comm == "shm" else "shm"
-        if alt == "rccl" and os.environ.get("SPX_BENCH_SAME_GPU") == "1":
-            xcomm = {"comm": alt, "skipped": "every rank on GPU 0: RCCL refuses two ranks on one device"}
-        else:
-            hub_x = attach(sctxs, alt)
-            batch_fn(sctxs, spk, 1)()
-            px, elx = timed(batch_fn(sctxs, spk, args.steps))
-            check_batch(px, ref)
-            xcomm = {"comm": alt, "elapsed": elx}
-            if hub_x is not None:
-                xcomm["hub_stats_rank0"] = hub_x.stats()
-                hub_x.close()  # the contexts keep it alive
     if hub is not None:
         hub_stats = hub.stats()
         hub.close()
@@ -755,7 +741,6 @@ def main():
     ms_1 = elapsed_single / args.steps * 1e3
     ms_1c = elapsed_single_c / args.steps * 1e3 if elapsed_single_c else 0.0
     ms_o = ms_o1 = None
-    ms_x = xcomm["elapsed"] / args.steps * 1e3 if xcomm and "elapsed" in xcomm else 0.0
     ms_g = {}
     if dist is not None:
         import torch
@@ -765,149 +750,193 @@ def main():
             dist.all_reduce(tg, op=dist.ReduceOp.MAX)
             ms_g[K] = float(tg[0])
         t = torch.tensor([ms, ms_c, ms_1, ms_1c, (other[0] / args.steps * 1e3) if other else 0.0,
-                          (other[1] / args.steps * 1e3) if other and other[1] else 0.0, ms_x], dtype=torch.float64)
+                          (other[1] / args.steps * 1e3) if other and other[1] else 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, ms_c, ms_1, ms_1c, ms_x = float(t[0]), float(t[1]), float(t[2]), float(t[3]), float(t[6])
+        ms, ms_c, ms_1, ms_1c = float(t[0]), float(t[1]), float(t[2]), float(t[3])
         if other:
             ms_o, ms_o1 = float(t[4]), (float(t[5]) or None)
     # whole-job throughput: in batch mode every rank proves P proofs per step, sharded all ranks share them
     jobs = P * (1 if sharded_head else world)
-    if rank != 0:
+    def make_out():  # rank 0: the JSON line
+        roof = None
+        if alone:
+            if stub:
+                roof = roofline_hbm(alone, PMC_FILE_C2 if log_n == 18 else None)
+            else:
+                dom = "msm_acc_g2" if "msm_acc_g2" in alone else max(alone, key=lambda k: alone[k]["ms"])
+                roof = roofline_valu(alone, dom)
+                if dom in stats:  # the same kernel while 16 proofs share the GPU
+                    d = stats[dom]
+                    roof["avg_launch_us_shared"] = round(d["ms"] / d["launches"] * 1e3, 2)
+                hb = roofline_hbm(alone, PMC_FILE if log_n == 20 else None)
+                if hb:
+                    roof["hbm_kernels"] = hb
+                if world == 1:
+                    wp = whole_proof_valu(ms / P)
+                    if wp:
+                        roof["whole_proof"] = wp
+        cpu = cpu_all = parity = None
+        if world == 1 and not args.no_cpu:
+            def gpu_pp_bytes(k):
+                # the GPU keygen's PP (seed 0xC0FFEE, as the oracle's keygen would make it), loaded into the
+                # oracle: a CPU keygen at 2^16+ would dominate the run
+                if k == log_n and pp is not None:
+                    return pp.serialize_uncompressed()
+                pp_s = spx.MLProofForR1CS.setup(ctx, k, 0xC0FFEE)
+                b = pp_s.serialize_uncompressed()
+                del pp_s
+                return b
+
+            one_log_n = args.cpu_log_n if not stub else 16
+            cpu = cpu_baseline(args.kind, one_log_n, log_v, args.cpu_seconds, stub=stub, max_reps=1,
+                               pp_bytes=None if stub else gpu_pp_bytes(one_log_n))
+            all_log_n = args.cpu_all_log_n if not stub else log_n
+            pp_bytes = None if stub else gpu_pp_bytes(all_log_n)
+            oracle_proof = []
+            cpu_all = cpu_baseline(args.kind, all_log_n, log_v, args.cpu_seconds, threads=host_cores(), pp_bytes=pp_bytes,
+                                   stub=stub, max_reps=1, out_proof=oracle_proof)
+            del pp_bytes
+            if all_log_n == log_n and args.kind == 3 and args.mode == "fs" and oracle_proof:
+                # the oracle just proved witness 0xB0B0 under the same index and PP: the GPU's ref[0]
+                parity = oracle_proof[0] == ref[0]
+                if not parity:
+                    sys.stderr.write("bench.py: PARITY FAILURE: the GPU proof differs from the oracle's at 2^%d\n" % log_n)
+        wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
+            KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
+            "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
+            args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, len(hctxs))
+        out = {
+            "metric": "R1CS constraints proved/sec at 2^%d%s" % (log_n, " (sumcheck-only, commitment stubbed)" if stub else ""),
+            "value": round(jobs * n / (ms / 1e3), 1),
+            "unit": "constraints/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            # --shard proof (default): the same proofs split over however many ranks (N = 1 included)
+            "scaling": "strong" if (sharded_head or (world == 1 and args.shard == "proof")) else "weak",
+            "vs_baseline": None,
+            "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
+            "data": "synthetic",
+            "config": {
+                "workload": wl,
+                "log_n": log_n,
+                "baseline_config": "C2" if stub else "C3",
+                "distinct_witnesses": W,
+                "proofs_per_step": P,
+                "proofs_in_flight": len(hctxs),
+                "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
+                "comm": args.comm if sctxs else None,
+            },
+            "ms_per_proof_single": round(ms_1, 3),
+            "value_single_proof": round(n / (ms_1 / 1e3), 1),
+            "ms_per_proof_single_cached_transcript": round(ms_1c, 3) if ms_1c else None,
+            "value_single_proof_cached_transcript": round(n / (ms_1c / 1e3), 1) if ms_1c else None,
+            "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1) if ms_c else None,
+            "ms_per_step_index_cached_transcript": round(ms_c, 3) if ms_c else None,
+            "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
+            "phases_ms_cached_transcript": {k: round(v / 1e3, 3) for k, v in phases_c.items()},
+            "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in alone.items()},
+            "kernels_ms_per_proof_shared": {k: round(v["ms"], 3) for k, v in stats.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
+            "setup_s": round(t_setup, 2),
+            "index_s": round(t_index, 2),
+            "gen_s": round(t_gen, 2),
+            "proof_bytes": len(ref[0]),
+            # the first witness's proof byte-equal to the test oracle's, proved in this run (cpu_baseline_all_cores)
+            "parity_2_%d" % log_n: parity,
+            "ranks_seen": ranks_seen,
+        }
+        if hub_stats is not None:
+            out["comm_%s_hub_stats_rank0" % args.comm] = hub_stats
+        # host side: the machine's cores, the ones this process uses, and how many of them the per-proof
+        # sequential Blake2s absorption of A, B, C keeps busy at the measured rate (proofs/s x seconds each)
+        # (the pool's own clock over the timed region: multi-buffer lanes hash several proofs per job)
+        hash_s = phases.get("transcript_matrices", 0.0) / 1e6
+        pool_s, pool_n = hs1[0] - hs0[0], hs1[1] - hs0[1]
+        out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
+                       "hashing_lanes": hs1[2],
+                       "hashing_core_s_per_proof": round(pool_s / pool_n, 4) if pool_n else None,
+                       "hashing_s_single_proof_scalar": round(hash_s, 4),
+                       "hashing_cores_busy": round(pool_s / elapsed, 2) if pool_n else 0.0}
+        for K, mg in ms_g.items():
+            out.setdefault("value_proof_groups", {})[str(K)] = {
+                "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),
+                "layout": "%d groups of %d ranks, every proof sharded over its group (%d proofs per group per step)" % (
+                    world // K, K, P)}
+        if ms_o is not None:
+            if sharded_head:  # the other mode: every rank proves whole proofs
+                out["value_batch_weak"] = round(P * world * n / (ms_o / 1e3), 1)
+                out["ms_per_step_batch_weak"] = round(ms_o, 3)
+            else:
+                out["value_proof_sharded"] = round(P * n / (ms_o / 1e3), 1)
+                out["ms_per_step_proof_sharded"] = round(ms_o, 3)
+                out["ms_per_proof_single_proof_sharded"] = round(ms_o1, 3) if ms_o1 else None
+        if rehearsal:
+            rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
+            out["proof_sharded_rehearsal"] = rehearsal
+        if not stub and world == 1 and not args.no_c2:
+            out["c2"] = c2_line(spx, L, args, Bb)
+        return out
+
+    out = make_out() if rank == 0 else None
+    # ---- N > 1, last: the same proof-sharded pipeline on the other transport (shm <-> RCCL over xGMI), so
+    # one run reports both. The contexts, index and witnesses stay; only their communicator changes. It
+    # runs after the headline is complete, under a watchdog: if the transport hangs (a collective that
+    # never completes), rank 0 prints the line without it after --comm-deadline seconds and every rank
+    # exits, so a failing second transport never costs the headline.
+    if sctxs and not args.one_comm:
+        alt = "rccl" if args.comm == "shm" else "shm"
+        if alt == "rccl" and os.environ.get("SPX_BENCH_SAME_GPU") == "1":
+            if out is not None:
+                out["value_comm_%s" % alt] = None
+                out["comm_%s_skipped" % alt] = "every rank on GPU 0: RCCL refuses two ranks on one device"
+        else:
+            import threading
+
+            def expire():
+                if out is not None:
+                    out["value_comm_%s" % alt] = None
+                    out["comm_%s_error" % alt] = "did not finish within %d s" % args.comm_deadline
+                    print(json.dumps(out), flush=True)
+                sys.stderr.flush()
+                os._exit(0)
+
+            dog = threading.Timer(args.comm_deadline, expire)
+            dog.daemon = True
+            dog.start()
+            try:
+                hub_x = attach(sctxs, alt)
+                batch_fn(sctxs, spk, 1)()
+                px, elx = timed(batch_fn(sctxs, spk, args.steps))
+                check_batch(px, ref)
+                err = None
+            except Exception as e:  # recorded; the other ranks' collectives end by the watchdog
+                hub_x, elx, err = None, 0.0, repr(e)
+            import torch
+
+            tx = torch.tensor([elx / args.steps * 1e3], dtype=torch.float64)
+            dist.all_reduce(tx, op=dist.ReduceOp.MAX)
+            dog.cancel()
+            if out is not None:
+                if err is None:
+                    ms_x = float(tx[0])
+                    out["value_comm_%s" % alt] = round(jobs * n / (ms_x / 1e3), 1)
+                    out["ms_per_step_comm_%s" % alt] = round(ms_x, 3)
+                    if hub_x is not None:
+                        out["comm_%s_hub_stats_rank0" % alt] = hub_x.stats()
+                else:
+                    out["value_comm_%s" % alt] = None
+                    out["comm_%s_error" % alt] = err
+            if hub_x is not None:
+                hub_x.close()  # the contexts keep it alive
+    if out is None:
         if dist is not None:
             dist.destroy_process_group()
         return
-
-    roof = None
-    if alone:
-        if stub:
-            roof = roofline_hbm(alone, PMC_FILE_C2 if log_n == 18 else None)
-        else:
-            dom = "msm_acc_g2" if "msm_acc_g2" in alone else max(alone, key=lambda k: alone[k]["ms"])
-            roof = roofline_valu(alone, dom)
-            if dom in stats:  # the same kernel while 16 proofs share the GPU
-                d = stats[dom]
-                roof["avg_launch_us_shared"] = round(d["ms"] / d["launches"] * 1e3, 2)
-            hb = roofline_hbm(alone, PMC_FILE if log_n == 20 else None)
-            if hb:
-                roof["hbm_kernels"] = hb
-            if world == 1:
-                wp = whole_proof_valu(ms / P)
-                if wp:
-                    roof["whole_proof"] = wp
-    cpu = cpu_all = parity = None
-    if world == 1 and not args.no_cpu:
-        def gpu_pp_bytes(k):
-            # the GPU keygen's PP (seed 0xC0FFEE, as the oracle's keygen would make it), loaded into the
-            # oracle: a CPU keygen at 2^16+ would dominate the run
-            if k == log_n and pp is not None:
-                return pp.serialize_uncompressed()
-            pp_s = spx.MLProofForR1CS.setup(ctx, k, 0xC0FFEE)
-            b = pp_s.serialize_uncompressed()
-            del pp_s
-            return b
-
-        one_log_n = args.cpu_log_n if not stub else 16
-        cpu = cpu_baseline(args.kind, one_log_n, log_v, args.cpu_seconds, stub=stub, max_reps=1,
-                           pp_bytes=None if stub else gpu_pp_bytes(one_log_n))
-        all_log_n = args.cpu_all_log_n if not stub else log_n
-        pp_bytes = None if stub else gpu_pp_bytes(all_log_n)
-        oracle_proof = []
-        cpu_all = cpu_baseline(args.kind, all_log_n, log_v, args.cpu_seconds, threads=host_cores(), pp_bytes=pp_bytes,
-                               stub=stub, max_reps=1, out_proof=oracle_proof)
-        del pp_bytes
-        if all_log_n == log_n and args.kind == 3 and args.mode == "fs" and oracle_proof:
-            # the oracle just proved witness 0xB0B0 under the same index and PP: the GPU's ref[0]
-            parity = oracle_proof[0] == ref[0]
-            if not parity:
-                sys.stderr.write("bench.py: PARITY FAILURE: the GPU proof differs from the oracle's at 2^%d\n" % log_n)
-    wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
-        KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
-        "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
-        args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, len(hctxs))
-    out = {
-        "metric": "R1CS constraints proved/sec at 2^%d%s" % (log_n, " (sumcheck-only, commitment stubbed)" if stub else ""),
-        "value": round(jobs * n / (ms / 1e3), 1),
-        "unit": "constraints/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms, 3),
-        "higher_is_better": True,
-        # --shard proof (default): the same proofs split over however many ranks (N = 1 included)
-        "scaling": "strong" if (sharded_head or (world == 1 and args.shard == "proof")) else "weak",
-        "vs_baseline": None,
-        "dtype": "bls12-381 Fr/Fq Montgomery (u32 limbs)",
-        "data": "synthetic",
-        "config": {
-            "workload": wl,
-            "log_n": log_n,
-            "baseline_config": "C2" if stub else "C3",
-            "distinct_witnesses": W,
-            "proofs_per_step": P,
-            "proofs_in_flight": len(hctxs),
-            "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
-            "comm": args.comm if sctxs else None,
-        },
-        "ms_per_proof_single": round(ms_1, 3),
-        "value_single_proof": round(n / (ms_1 / 1e3), 1),
-        "ms_per_proof_single_cached_transcript": round(ms_1c, 3) if ms_1c else None,
-        "value_single_proof_cached_transcript": round(n / (ms_1c / 1e3), 1) if ms_1c else None,
-        "value_index_cached_transcript": round(jobs * n / (ms_c / 1e3), 1) if ms_c else None,
-        "ms_per_step_index_cached_transcript": round(ms_c, 3) if ms_c else None,
-        "phases_ms": {k: round(v / 1e3, 3) for k, v in phases.items()},
-        "phases_ms_cached_transcript": {k: round(v / 1e3, 3) for k, v in phases_c.items()},
-        "kernels_ms_per_proof": {k: round(v["ms"], 3) for k, v in alone.items()},
-        "kernels_ms_per_proof_shared": {k: round(v["ms"], 3) for k, v in stats.items()},
-        "roofline": roof,
-        "cpu_baseline": cpu,
-        "cpu_baseline_all_cores": cpu_all,
-        "setup_s": round(t_setup, 2),
-        "index_s": round(t_index, 2),
-        "gen_s": round(t_gen, 2),
-        "proof_bytes": len(ref[0]),
-        # the first witness's proof byte-equal to the test oracle's, proved in this run (cpu_baseline_all_cores)
-        "parity_2_%d" % log_n: parity,
-        "ranks_seen": ranks_seen,
-    }
-    if xcomm is not None:
-        if "elapsed" in xcomm:
-            out["value_comm_%s" % xcomm["comm"]] = round(jobs * n / (ms_x / 1e3), 1)
-            out["ms_per_step_comm_%s" % xcomm["comm"]] = round(ms_x, 3)
-            if "hub_stats_rank0" in xcomm:
-                out["comm_%s_hub_stats_rank0" % xcomm["comm"]] = xcomm["hub_stats_rank0"]
-        else:
-            out["value_comm_%s" % xcomm["comm"]] = None
-            out["comm_%s_skipped" % xcomm["comm"]] = xcomm["skipped"]
-    if hub_stats is not None:
-        out["comm_%s_hub_stats_rank0" % args.comm] = hub_stats
-    # host side: the machine's cores, the ones this process uses, and how many of them the per-proof
-    # sequential Blake2s absorption of A, B, C keeps busy at the measured rate (proofs/s x seconds each)
-    # (the pool's own clock over the timed region: multi-buffer lanes hash several proofs per job)
-    hash_s = phases.get("transcript_matrices", 0.0) / 1e6
-    pool_s, pool_n = hs1[0] - hs0[0], hs1[1] - hs0[1]
-    out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
-                   "hashing_lanes": hs1[2],
-                   "hashing_core_s_per_proof": round(pool_s / pool_n, 4) if pool_n else None,
-                   "hashing_s_single_proof_scalar": round(hash_s, 4),
-                   "hashing_cores_busy": round(pool_s / elapsed, 2) if pool_n else 0.0}
-    for K, mg in ms_g.items():
-        out.setdefault("value_proof_groups", {})[str(K)] = {
-            "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),
-            "layout": "%d groups of %d ranks, every proof sharded over its group (%d proofs per group per step)" % (
-                world // K, K, P)}
-    if ms_o is not None:
-        if sharded_head:  # the other mode: every rank proves whole proofs
-            out["value_batch_weak"] = round(P * world * n / (ms_o / 1e3), 1)
-            out["ms_per_step_batch_weak"] = round(ms_o, 3)
-        else:
-            out["value_proof_sharded"] = round(P * n / (ms_o / 1e3), 1)
-            out["ms_per_step_proof_sharded"] = round(ms_o, 3)
-            out["ms_per_proof_single_proof_sharded"] = round(ms_o1, 3) if ms_o1 else None
-    if rehearsal:
-        rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
-        out["proof_sharded_rehearsal"] = rehearsal
-    if not stub and world == 1 and not args.no_c2:
-        out["c2"] = c2_line(spx, L, args, Bb)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

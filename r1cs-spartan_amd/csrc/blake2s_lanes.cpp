@@ -145,21 +145,24 @@ void blake2s_update_lanes(Blake2s* st, int k, const void* data, size_t len) {
         for (int l = 0; l < k; ++l) st[l].update(p, len);
         return;
     }
-    for (int l = 0; l < k; l += w) {
-        // a short last group runs at full width on copies (the extra lanes' results are dropped)
+    for (int l = 0; l < k;) {
+        // groups of 16 (AVX-512) while at least 9 states remain, then 8 (AVX2, also on AVX-512
+        // machines); a short last group runs at full width on copies (the extra lanes are dropped)
+        const int gw = (w == 16 && k - l > 8) ? 16 : 8;
         Blake2s tmp[16];
-        const int n = std::min(w, k - l);
+        const int n = std::min(gw, k - l);
         Blake2s* g = st + l;
-        if (n < w) {
-            for (int i = 0; i < w; ++i) tmp[i] = st[l + std::min(i, n - 1)];
+        if (n < gw) {
+            for (int i = 0; i < gw; ++i) tmp[i] = st[l + std::min(i, n - 1)];
             g = tmp;
         }
-        if (w == 16)
+        if (gw == 16)
             Blake2sLanes::update16(g, p, len);
         else
             Blake2sLanes::update8(g, p, len);
-        if (n < w)
+        if (n < gw)
             for (int i = 0; i < n; ++i) st[l + i] = tmp[i];
+        l += n;
     }
 }
 

@@ -417,15 +417,24 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     // A job absorbs A, B, C for `lanes` consecutive proofs at once: multi-buffer BLAKE2s, one proof's
     // state per vector lane (blake2s_lanes.cpp; 16 lanes with AVX-512, 8 with AVX2). Every proof's
     // transcript still absorbs the matrices itself (lib.rs:61-64); the lanes share the instructions.
+    // The first in-flight proofs wait for their absorption before their first challenge, and a
+    // 16-lane (AVX-512) job takes ~1.8x one scalar absorption on the GPU box's cores: the jobs covering
+    // the first nctx owned proofs use 8 lanes (about one scalar absorption's time), the rest full width.
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
-    const size_t njobs = (owned.size() + lanes - 1) / lanes;
+    std::vector<std::pair<size_t, size_t>> jobs;
+    for (size_t b = 0; b < owned.size();) {
+        const size_t w = (lanes == 16 && b < (size_t)nctx) ? 8 : (size_t)lanes;
+        jobs.emplace_back(b, std::min(owned.size(), b + w));
+        b += w;
+    }
+    const size_t njobs = jobs.size();
     auto hasher = [&] {
         std::vector<spx::Blake2s> tmp(lanes);
         for (;;) {
             const size_t j = next_job.fetch_add(1);
             if (j >= njobs) return;
-            const size_t b = j * lanes, e = std::min(owned.size(), b + lanes);
+            const size_t b = jobs[j].first, e = jobs[j].second;
             int st = 1;
             try {
                 const auto t0 = clk::now();

@@ -187,6 +187,24 @@ DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
         fq_mul_asm(r, a, b);
 }
 
+// two independent Fr products: one instruction stream carrying both multiply-accumulate chains
+// (ff_asm.hpp fr_mul_x2_asm). Every Fr kernel is bound by the dependent chain of one product
+// (DESIGN.md 4.3), so a wave with two products in flight issues twice the independent work.
+#ifndef SPX_FR_X2
+#define SPX_FR_X2 1
+#endif
+DEV void fr_mul_pair(Fr& r0, const Fr& a0, const Fr& b0, Fr& r1, const Fr& a1, const Fr& b1) {
+#if SPX_FR_X2
+    fr_mul_x2_asm(r0, a0, b0, r1, a1, b1);
+#else
+    Fr t0, t1;
+    fr_mul_asm(t0, a0, b0);
+    fr_mul_asm(t1, a1, b1);
+    r0 = t0;
+    r1 = t1;
+#endif
+}
+
 template <class C>
 DEV void fe_sqr(Fe<C>& r, const Fe<C>& a) {
     fe_mul(r, a, a);

@@ -255,10 +255,8 @@ __global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFac
             Fr v0 = ld_fr(vp + (size_t)j * 64), v1 = ld_fr(vp + (size_t)(j + 1) * 64);
             Fr a0 = ld_fr(lo + (r0 & mask)), a1 = ld_fr(lo + (r1 & mask));
             Fr b0 = ld_fr(hi3 + hidx(r0)), b1 = ld_fr(hi3 + hidx(r1)), t0, t1;
-            fe_mul(t0, v0, a0);
-            fe_mul(t1, v1, a1);
-            fe_mul(t0, t0, b0);
-            fe_mul(t1, t1, b1);
+            fr_mul_pair(t0, v0, a0, t1, v1, a1);
+            fr_mul_pair(t0, t0, b0, t1, t1, b1);
             fe_add(acc, acc, t0);
             fe_add(acc, acc, t1);
         }
@@ -666,13 +664,12 @@ DEV void wave_fold(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t bas
     uint4 a[8];
     wave_rows_in<8>(reinterpret_cast<const uint4*>(in + 4 * base), lds, a, lane);
     const Fr a0 = fr_of(a[0], a[1]), a1 = fr_of(a[2], a[3]), a2 = fr_of(a[4], a[5]), a3 = fr_of(a[6], a[7]);
-    Fr d;
-    fe_sub(d, a1, a0);
-    fe_mul(d, d, r);
-    fe_add(x0, a0, d);
-    fe_sub(d, a3, a2);
-    fe_mul(d, d, r);
-    fe_add(x1, a2, d);
+    Fr d0, d1;
+    fe_sub(d0, a1, a0);
+    fe_sub(d1, a3, a2);
+    fr_mul_pair(d0, d0, r, d1, d1, r);
+    fe_add(x0, a0, d0);
+    fe_add(x1, a2, d1);
     uint4 o[4];
     fr_to(o[0], o[1], x0);
     fr_to(o[2], o[3], x1);
@@ -721,26 +718,25 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, 
             wave_rows_in<2>(reinterpret_cast<const uint4*>(Ein + base), lds, ev, lane);
             e = fr_of(ev[0], ev[1]);
         }
-        Fr t, u, y[3];
-        fe_mul(t, x0[0], x0[1]);
+        Fr t, t2, u, y[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            fe_add(u, x1[m], x1[m]);
+            fe_sub(y[m], u, x0[m]);
+        }
+        // G(0) and G(2) terms as product pairs (two independent chains per wave)
+        fr_mul_pair(t, x0[0], x0[1], t2, y[0], y[1]);
         fe_sub(t, t, x0[2]);
-        fe_mul(t, t, e);
+        fe_sub(t2, t2, y[2]);
+        fr_mul_pair(t, t, e, t2, t2, e);
         fe_add(g[0], g[0], t);
+        fe_add(g[2], g[2], t2);
         if constexpr (NEED1) {
             fe_mul(t, x1[0], x1[1]);
             fe_sub(t, t, x1[2]);
             fe_mul(t, t, e);
             fe_add(g[1], g[1], t);
         }
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            fe_add(u, x1[m], x1[m]);
-            fe_sub(y[m], u, x0[m]);
-        }
-        fe_mul(t, y[0], y[1]);
-        fe_sub(t, t, y[2]);
-        fe_mul(t, t, e);
-        fe_add(g[2], g[2], t);
     }
     if constexpr (FUSED)
         grid_reduce_last<3>(g, partial, ticket, result3);
@@ -771,18 +767,18 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __
             wave_pair(Min, base, lds, lane, m0, m1);
             wave_pair(Zin, base, lds, lane, z0, z1);
         }
-        fe_mul(t, m0, z0);
-        fe_add(g[0], g[0], t);
-        if constexpr (NEED1) {
-            fe_mul(t, m1, z1);
-            fe_add(g[1], g[1], t);
-        }
+        Fr t2;
         fe_add(u, m1, m1);
         fe_sub(u, u, m0);
         fe_add(v, z1, z1);
         fe_sub(v, v, z0);
-        fe_mul(t, u, v);
-        fe_add(g[2], g[2], t);
+        fr_mul_pair(t, m0, z0, t2, u, v);
+        fe_add(g[0], g[0], t);
+        fe_add(g[2], g[2], t2);
+        if constexpr (NEED1) {
+            fe_mul(t, m1, z1);
+            fe_add(g[1], g[1], t);
+        }
     }
     if constexpr (FUSED)
         grid_reduce_last<3>(g, partial, ticket, result3);
@@ -908,12 +904,12 @@ DEV void fold_group4(const uint4 (&a)[8], const FoldArgs<3>& fa, int j0, Fr (&q0
     Fr v[4], t;
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = fr_of(a[2 * k], a[2 * k + 1]);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        fe_sub(q0[k], v[2 * k + 1], v[2 * k]);
-        fe_mul(t, q0[k], fa.p[j0]);
-        fe_add(v[k], v[2 * k], t);
-    }
+    Fr t1;
+    fe_sub(q0[0], v[1], v[0]);
+    fe_sub(q0[1], v[3], v[2]);
+    fr_mul_pair(t, q0[0], fa.p[j0], t1, q0[1], fa.p[j0]);  // the level's two folds: one pair
+    fe_add(v[0], v[0], t);
+    fe_add(v[1], v[2], t1);
     fe_sub(q1, v[1], v[0]);
     fe_mul(t, q1, fa.p[j0 + 1]);
     fe_add(u, v[0], t);

@@ -1110,6 +1110,13 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         return e && std::string(e) == "batch";
     }();
     const bool lvl0_batch = C.lvl0_mode >= 0 ? C.lvl0_mode == 1 : lvl0_batch_env;
+    // SPX_CHECK_DERIVED=1 (tests): from round 2 on, a sumcheck round's value at 1 is derived from the
+    // previous claim on the host (P(0) + P(1) = claim); with this set the device computes it too and the
+    // prove fails with SPX_SUMCHECK if they differ (the identity pinned round by round, every rank count)
+    const bool check_derived = [] {
+        const char* e = getenv("SPX_CHECK_DERIVED");
+        return e && e[0] == '1';
+    }();
     if (G > 1 && !C.knobs_agreed) {
         // the level-0 mode decides the order and sizes of a proof's exchanges: every rank of the
         // communicator must read the same SPX_LVL0 (one exchange on a context's first sharded proof)
@@ -1230,7 +1237,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         const HFr ct = Cc * tau[i - 1];
         const bool derive1 = fold && !ct.is_zero();
         launch_sc1_round(fold, cur, out, Ecur, Eout, fold ? dev_fr(r_x[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
-                         !derive1, C.stream);
+                         !derive1 || check_derived, C.stream);
         C.sync();
         HFr gs[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1239,7 +1246,12 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             for (int r = 0; r < G; ++r)
                 for (int k = 0; k < 3; ++k) gs[k] += all[3 * r + k];
         }
-        if (derive1) gs[1] = (claim1 - (Cc - ct) * gs[0]) * ct.inv();
+        if (derive1) {
+            const HFr d1 = (claim1 - (Cc - ct) * gs[0]) * ct.inv();
+            if (check_derived && !(d1 == gs[1]))
+                throw SpxError(kSumcheck, "sumcheck 1 round " + std::to_string(i) + ": derived G(1) differs from the device's");
+            gs[1] = d1;
+        }
         std::vector<HFr> msg = sc1_message(Cc, tau[i - 1], gs, L);
         size_t m0 = proof.b.size();
         proof.u64(msg.size());
@@ -1352,7 +1364,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         Fr* Zo = fold ? Zb[i & 1] : nullptr;
         // from round 2 on, P(1) = claim - P(0) (the folded tables' identity): the kernel skips it
         launch_sc2_round(fold, Mc, Zc, Mo, Zo, fold ? dev_fr(r_y[i - 2]) : Fr{}, half, partial, C.ticket, res_dev,
-                         !fold, C.stream);
+                         !fold || check_derived, C.stream);
         C.sync();
         HFr ps[3] = {ld_hfr(hp), ld_hfr(hp + 32), ld_hfr(hp + 64)};
         if (G > 1) {
@@ -1361,7 +1373,12 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             for (int r = 0; r < G; ++r)
                 for (int k = 0; k < 3; ++k) ps[k] += all[3 * r + k];
         }
-        if (fold) ps[1] = claim2 - ps[0];
+        if (fold) {
+            const HFr d1 = claim2 - ps[0];
+            if (check_derived && !(d1 == ps[1]))
+                throw SpxError(kSumcheck, "sumcheck 2 round " + std::to_string(i) + ": derived P(1) differs from the device's");
+            ps[1] = d1;
+        }
         size_t m0 = proof.b.size();
         proof.u64(3);
         for (int k = 0; k < 3; ++k) proof.fr(ps[k]);

@@ -131,3 +131,42 @@ def test_virtual_ranks_level0_mode_mismatch(spx, oc):
     with pytest.raises(AssertionError) as e:
         _prove_ranks(spx, G, inst, ppb, lvl0=[1, 0])
     assert "level-0 mode differs" in str(e.value)
+
+
+@pytest.mark.parametrize("G", [1, 2, 4])
+def test_derived_round_values_match_device(spx, oc, G):
+    """From round 2 on a sumcheck round's value at 1 is derived on the host from the previous claim
+    (prover.cpp). SPX_CHECK_DERIVED=1 makes the device compute it as well and fails the prove
+    (SPX_SUMCHECK) on any difference: the identity is checked round by round, unsharded and over
+    G virtual ranks, and the proof stays equal to the oracle's."""
+    import threading
+
+    log_n, log_v = 10, 3
+    inst = oc.Instance(0, log_n, log_v, 808)
+    ppc = oc.PP.keygen(log_n, 809)
+    want = oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
+    os.environ["SPX_CHECK_DERIVED"] = "1"
+    try:
+        group = spx.CommGroup(G) if G > 1 else None
+        out, errs = [None] * G, []
+
+        def rank(r):
+            try:
+                c = spx.Context(0)
+                if group is not None:
+                    c.set_comm_group(group, r)
+                pp = spx.PublicParameter.load(c, ppc.serialize())
+                pk = spx.MLArgumentForR1CS.index(c, *[spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats])
+                out[r] = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+            except Exception as e:
+                errs.append(repr(e))
+
+        ths = [threading.Thread(target=rank, args=(r,)) for r in range(G)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=300)
+    finally:
+        del os.environ["SPX_CHECK_DERIVED"]
+    assert not errs, errs
+    assert all(o == want for o in out)

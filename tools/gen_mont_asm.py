@@ -10,6 +10,10 @@ Column k of the 2N-1 columns (Koc et al., FIPS):
   k >= N: r_{k-N} = lo(acc)
   acc >>= 32
 Result < 2p (spare top bits), one conditional subtraction.
+
+fr_mul_x2_asm: two independent Fr products whose chains are interleaved instruction by instruction
+(the second chain's carries in an SGPR pair instead of VCC), so one wave has two independent
+multiply-accumulate chains in flight: the Fr kernels are bound by the dependent chain.
 """
 import os
 
@@ -81,6 +85,65 @@ def gen(name, N, p):
     return "\n".join(L)
 
 
+def gen_x2(name, N, p):
+    P = limbs(p, N)
+    inv = (-pow(p, -1, 1 << 32)) % (1 << 32)
+    assert P[0] == 1 and inv == 0xFFFFFFFF  # Fr shortcut only
+    L = []
+    L.append("// %s: two independent products, their multiply-accumulate chains interleaved instruction by" % name)
+    L.append("// instruction (carries in VCC and in an SGPR pair): twice the independent work per wave")
+    L.append("DEV void %s_mul_x2_asm(Fe<%sCfg>& r0, const Fe<%sCfg>& A0, const Fe<%sCfg>& B0, Fe<%sCfg>& r1," % (name.lower(), name, name, name, name))
+    L.append("                          const Fe<%sCfg>& A1, const Fe<%sCfg>& B1) {" % (name, name))
+    L.append("    const uint32_t *a = A0.v, *b = B0.v, *c = A1.v, *d = B1.v;")
+    L.append("    uint32_t m[%d], n[%d], t[%d], u[%d];" % (N, N, N, N))
+    L.append("    uint64_t acc = 0, acd = 0, cs;")
+    L.append("    uint32_t top, tpd;")
+    for k in range(2 * N - 1):
+        terms = []
+        for i in range(max(0, k - N + 1), min(k, N - 1) + 1):
+            terms.append(("ab", i, k - i))
+        for i in range(max(0, k - N + 1), min(k - 1, N - 1) + 1):
+            terms.append(("mp", i, k - i))
+        L.append("    top = 0;")
+        L.append("    tpd = 0;")
+        if terms:
+            lines = []
+            ins = {}
+            for (kind, i, j) in terms:
+                if kind == "ab":
+                    x0, y0, x1, y1 = "a%d" % i, "b%d" % j, "c%d" % i, "d%d" % j
+                    ins[x0] = '"v"(a[%d])' % i; ins[y0] = '"v"(b[%d])' % j
+                    ins[x1] = '"v"(c[%d])' % i; ins[y1] = '"v"(d[%d])' % j
+                else:
+                    x0, y0, x1, y1 = "m%d" % i, "p%d" % j, "n%d" % i, "p%d" % j
+                    ins[x0] = '"v"(m[%d])' % i; ins[x1] = '"v"(n[%d])' % i
+                    ins[y0] = '"s"(0x%08xu)' % P[j]
+                lines.append('"v_mad_u64_u32 %%[acc], vcc, %%[%s], %%[%s], %%[acc]\\n\\t"' % (x0, y0))
+                lines.append('"v_mad_u64_u32 %%[acd], %%[cs], %%[%s], %%[%s], %%[acd]\\n\\t"' % (x1, y1))
+                lines.append('"v_addc_co_u32 %[top], vcc, 0, %[top], vcc\\n\\t"')
+                lines.append('"v_addc_co_u32 %[tpd], %[cs], 0, %[tpd], %[cs]\\n\\t"')
+            L.append("    asm(" + "\n        ".join(lines))
+            L.append('        : [acc] "+v"(acc), [top] "+v"(top), [acd] "+v"(acd), [tpd] "+v"(tpd), [cs] "=&s"(cs)')
+            L.append("        : " + ", ".join("[%s] %s" % (nm, cst) for nm, cst in ins.items()))
+            L.append('        : "vcc");')
+        if k < N:
+            L.append("    m[%d] = 0u - (uint32_t)acc;" % k)
+            L.append("    acc = (acc >> 32) + ((uint64_t)top << 32) + (uint64_t)((uint32_t)acc != 0u);")
+            L.append("    n[%d] = 0u - (uint32_t)acd;" % k)
+            L.append("    acd = (acd >> 32) + ((uint64_t)tpd << 32) + (uint64_t)((uint32_t)acd != 0u);")
+            continue
+        L.append("    t[%d] = (uint32_t)acc;" % (k - N))
+        L.append("    acc = (acc >> 32) | ((uint64_t)top << 32);")
+        L.append("    u[%d] = (uint32_t)acd;" % (k - N))
+        L.append("    acd = (acd >> 32) | ((uint64_t)tpd << 32);")
+    L.append("    t[%d] = (uint32_t)acc;" % (N - 1))
+    L.append("    u[%d] = (uint32_t)acd;" % (N - 1))
+    L.append("    fe_reduce_once<%sCfg>(r0, t);" % name)
+    L.append("    fe_reduce_once<%sCfg>(r1, u);" % name)
+    L.append("}")
+    return "\n".join(L)
+
+
 def main():
     out = [
         "// GENERATED by tools/gen_mont_asm.py — do not edit.",
@@ -93,6 +156,8 @@ def main():
     for name, (N, p) in MODS.items():
         out.append(gen(name, N, p))
         out.append("")
+    out.append(gen_x2("Fr", *MODS["Fr"]))
+    out.append("")
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "r1cs-spartan_amd", "csrc", "ff_asm.hpp")
     open(path, "w").write("\n".join(out) + "\n")
 

@@ -188,21 +188,11 @@ DEV void fe_mul(Fe<C>& r, const Fe<C>& a, const Fe<C>& b) {
 }
 
 // two independent Fr products: one instruction stream carrying both multiply-accumulate chains
-// (ff_asm.hpp fr_mul_x2_asm). Every Fr kernel is bound by the dependent chain of one product
-// (DESIGN.md 4.3), so a wave with two products in flight issues twice the independent work.
-#ifndef SPX_FR_X2
-#define SPX_FR_X2 1
-#endif
+// (ff_asm.hpp fr_mul_x2_asm). At 8 waves per SIMD one chain already issues at the VALU rate
+// (tools/ubench_frmul.hip: 1175 vs 1171 cycles per product); the pair helps where a kernel runs
+// fewer waves or stalls on loads (k_col_stream 167 -> 150 us; profiles/r04/r04q_ab.jsonl).
 DEV void fr_mul_pair(Fr& r0, const Fr& a0, const Fr& b0, Fr& r1, const Fr& a1, const Fr& b1) {
-#if SPX_FR_X2
     fr_mul_x2_asm(r0, a0, b0, r1, a1, b1);
-#else
-    Fr t0, t1;
-    fr_mul_asm(t0, a0, b0);
-    fr_mul_asm(t1, a1, b1);
-    r0 = t0;
-    r1 = t1;
-#endif
 }
 
 template <class C>

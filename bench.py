@@ -609,12 +609,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def timed(fn):
+    cpu_busy = {}  # this process's CPU seconds (all threads) per second of a timed run, by label
+
+    def timed(fn, label=None):
         barrier()
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.process_time()
         r = fn()
+        c1 = time.process_time()
         barrier()
-        return r, time.perf_counter() - t0
+        el = time.perf_counter() - t0
+        if label:
+            cpu_busy[label] = round((c1 - c0) / el, 2)
+        return r, el
 
     def batch_fn(cs, k, steps, cached=False):
         wl = [wits[i % W] for i in range(P * steps)]
@@ -643,7 +649,7 @@ def main():
         spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
     # ---- timed region (headline): K steps x P full proofs, pipelined over B workers
     hs0 = spx.hash_stats()
-    proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps))
+    proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps), "headline")
     hs1 = spx.hash_stats()
     stats = {}
     if not args.no_stats:
@@ -670,7 +676,7 @@ def main():
         phases_c = hctx.last_timings()
     # ---- index-cached transcript throughput (matrix absorption moved to index time; bit-identical)
     if not args.no_cached:
-        p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True))
+        p2, elapsed_cached = timed(batch_fn(hctxs, hpk, args.steps, cached=True), "index_cached")
         check_batch(p2, ref)
     # ---- N > 1: the other shard mode (throughput, and the proof-sharded single-proof latency)
     other = None
@@ -861,7 +867,11 @@ def main():
                        "hashing_lanes": hs1[2],
                        "hashing_core_s_per_proof": round(pool_s / pool_n, 4) if pool_n else None,
                        "hashing_s_single_proof_scalar": round(hash_s, 4),
-                       "hashing_cores_busy": round(pool_s / elapsed, 2) if pool_n else 0.0}
+                       "hashing_cores_busy": round(pool_s / elapsed, 2) if pool_n else 0.0,
+                       # summed over the proof workers: time a proof waited for its absorption
+                       "hashing_wait_ms_per_proof": round((hs1[3] - hs0[3]) / pool_n * 1e3, 2) if pool_n else None,
+                       # the whole process's CPU use (proof workers, HIP runtime, hashing pool) in cores
+                       "process_cores_busy": cpu_busy}
         for K, mg in ms_g.items():
             out.setdefault("value_proof_groups", {})[str(K)] = {
                 "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),

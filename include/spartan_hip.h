@@ -188,8 +188,9 @@ int spx_prover_free(spx_prover *p);
 
 /* host time spent by spx_prove_many's hashing pools absorbing A, B, C (lib.rs:61-64), process-wide:
  * out[0] nanoseconds (summed over the pool threads), out[1] proofs absorbed, out[2] the multi-buffer
- * lane width (proofs hashed per vector instruction: 16 AVX-512, 8 AVX2, 1 scalar) */
-int spx_hash_stats(uint64_t out[3]);
+ * lane width (proofs hashed per vector instruction: 16 AVX-512, 8 AVX2, 1 scalar), out[3] nanoseconds
+ * the proof workers waited for a proof's absorption (summed over the workers) */
+int spx_hash_stats(uint64_t out[4]);
 /* MLArgumentForR1CS::verify (src/lib.rs:147-212, verifier.rs:143-512): SPX_OK = accepted (the
  * reference's Ok(true)); a rejection returns the reference's error kind (SPX_INVALID_ARGUMENT,
  * SPX_SUMCHECK, SPX_WRONG_WITNESS, SPX_SERIALIZATION) with its message in spx_last_error.

@@ -447,10 +447,11 @@ class ExchangeHub:
 
 
 def hash_stats():
-    """(seconds, proofs, lane width) of spx_prove_many's matrix absorption so far (process-wide)"""
-    out = (ctypes.c_uint64 * 3)()
+    """(seconds, proofs, lane width, seconds the proof workers waited for an absorption) of
+    spx_prove_many's matrix absorption so far (process-wide)"""
+    out = (ctypes.c_uint64 * 4)()
     _check(lib().spx_hash_stats(out))
-    return out[0] / 1e9, out[1], out[2]
+    return out[0] / 1e9, out[1], out[2], out[3] / 1e9
 
 
 def shm_name():

@@ -151,6 +151,12 @@ void blake2s_update_lanes(Blake2s* st, int k, const void* data, size_t len) {
         const int gw = (w == 16 && k - l > 8) ? 16 : 8;
         Blake2s tmp[16];
         const int n = std::min(gw, k - l);
+        if (n <= 2) {  // one or two states: scalar streams (a padded vector group costs more, and the
+                       // scalar code shares a core's SMT siblings far better; spx_prove_many's first waves)
+            for (int i = 0; i < n; ++i) st[l + i].update(p, len);
+            l += n;
+            continue;
+        }
         Blake2s* g = st + l;
         if (n < gw) {
             for (int i = 0; i < gw; ++i) tmp[i] = st[l + std::min(i, n - 1)];

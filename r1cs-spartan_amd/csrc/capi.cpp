@@ -14,6 +14,7 @@
 #include <thread>
 #include <vector>
 
+#include "hash_sched.hpp"
 #include "interactive.hpp"
 #include "pairing.hpp"
 #include "prover.hpp"
@@ -43,7 +44,7 @@ struct spx_prover {
 namespace {
 thread_local std::string g_err;
 // host time spent absorbing A, B, C in spx_prove_many's hashing pools, and the proofs absorbed
-std::atomic<uint64_t> g_hash_ns{0}, g_hash_proofs{0};
+std::atomic<uint64_t> g_hash_ns{0}, g_hash_proofs{0}, g_hash_wait_ns{0};
 template <class F>
 int guard(F&& f) {
     try {
@@ -412,29 +413,25 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             if (i % G == rank) owned.push_back(i);
     std::mutex mu;
     std::condition_variable cv;
-    std::atomic<size_t> next_job{0};
     std::string pool_err;
     // A job absorbs A, B, C for `lanes` consecutive proofs at once: multi-buffer BLAKE2s, one proof's
     // state per vector lane (blake2s_lanes.cpp; 16 lanes with AVX-512, 8 with AVX2). Every proof's
     // transcript still absorbs the matrices itself (lib.rs:61-64); the lanes share the instructions.
-    // The first in-flight proofs wait for their absorption before their first challenge, and a
-    // 16-lane (AVX-512) job takes ~1.8x one scalar absorption on the GPU box's cores: the jobs covering
-    // the first nctx owned proofs use 8 lanes (about one scalar absorption's time), the rest full width.
+    // Schedule (hash_sched.hpp). The first in-flight proofs wait for their absorption before their
+    // first challenge: one scalar absorption takes 0.15-0.17 s, a full-width job ~0.3 s at best, so
+    // with full-width jobs from the start the early waves of proofs waited for theirs (34 ms per proof
+    // and 56.2 vs 59.6-60.3 M constraints/s for an all-scalar pool; profiles/r04/r04u_ab_hash_wait.jsonl).
+    // The first two waves are scalar; a few full-width jobs for the next waves start beside them.
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
-    std::vector<std::pair<size_t, size_t>> jobs;
-    for (size_t b = 0; b < owned.size();) {
-        const size_t w = (lanes == 16 && b < (size_t)nctx) ? 8 : (size_t)lanes;
-        jobs.emplace_back(b, std::min(owned.size(), b + w));
-        b += w;
-    }
-    const size_t njobs = jobs.size();
+    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes);  // hash_sched.hpp
+    const size_t njobs = sched.size();
     auto hasher = [&] {
         std::vector<spx::Blake2s> tmp(lanes);
         for (;;) {
-            const size_t j = next_job.fetch_add(1);
+            const size_t j = sched.claim();
             if (j >= njobs) return;
-            const size_t b = jobs[j].first, e = jobs[j].second;
+            const size_t b = sched.jobs[j].first, e = sched.jobs[j].second;
             int st = 1;
             try {
                 const auto t0 = clk::now();
@@ -462,7 +459,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     int budget = (int)std::thread::hardware_concurrency();
     if (const char* e = getenv("OMP_NUM_THREADS")) budget = atoi(e);
     budget = std::max(1, budget);
-    int nh = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
+    int nh = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget) + (int)sched.nlead;
     if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
     nh = std::min<int>(nh, (int)njobs);
     std::vector<std::thread> pool;
@@ -478,8 +475,10 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
                 o.seq = i;
                 if (!base.cached && i % G == rank)  // waited for inside prove, behind the proof's first kernels
                     o.await_absorbed = [&, i]() -> const spx::Blake2s* {
+                        const auto w0 = clk::now();
                         std::unique_lock<std::mutex> lk(mu);
                         cv.wait(lk, [&] { return slots[i].state.load() != 0; });
+                        g_hash_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - w0).count();
                         if (slots[i].state.load() == 2)
                             throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
                         return &slots[i].h;
@@ -501,7 +500,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     for (int k = 1; k < nw; ++k) th.emplace_back(work, k);
     work(0);
     for (auto& t : th) t.join();
-    next_job.store(njobs);  // stop a pool still running after a worker failure
+    sched.stop();  // stop a pool still running after a worker failure
     for (auto& t : pool) t.join();
     for (int k = 0; k < nw; ++k)
         if (st[k] != SPX_OK) {
@@ -511,12 +510,13 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     g_err.clear();
     return SPX_OK;
 }
-int spx_hash_stats(uint64_t out[3]) {
+int spx_hash_stats(uint64_t out[4]) {
     return guard([&] {
         if (!out) spx::invalid("null argument");
         out[0] = g_hash_ns.load();
         out[1] = g_hash_proofs.load();
         out[2] = (uint64_t)std::max(1, spx::blake2s_lane_width());
+        out[3] = g_hash_wait_ns.load();
     });
 }
 int spx_vp_from_pp(spx_pp* pp, uint8_t* out, size_t cap, size_t* len) {

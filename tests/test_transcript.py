@@ -48,3 +48,17 @@ def test_blake2s_lanes_match_scalar(tmp_path):
     out = subprocess.check_output([exe], timeout=300).decode()
     assert out.startswith("ok"), out
     print(out)
+
+
+def test_hash_pool_schedule(tmp_path):
+    """spx_prove_many's hashing-pool plan (csrc/hash_sched.hpp): every owned proof absorbed exactly once
+    for any pool size / context count / lane width, the first two waves one proof per job, and every
+    pool thread terminates"""
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if not cxx:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path / "hsched")
+    subprocess.check_call([cxx, "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "r1cs-spartan_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "hash_sched_check.cpp"), "-o", exe])
+    out = subprocess.check_output([exe], timeout=300).decode()
+    assert out.startswith("ok"), out

@@ -421,10 +421,12 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     // first challenge: one scalar absorption takes 0.15-0.17 s, a full-width job ~0.3 s at best, so
     // with full-width jobs from the start the early waves of proofs waited for theirs (34 ms per proof
     // and 56.2 vs 59.6-60.3 M constraints/s for an all-scalar pool; profiles/r04/r04u_ab_hash_wait.jsonl).
-    // The first two waves are scalar; a few full-width jobs for the next waves start beside them.
+    // The first two waves are scalar; a few full-width jobs for the next waves start beside them. With
+    // the commitment stubbed (C2), all full width: 277 -> 370 M constraints/s at 2^18 in the same A/B
+    // (profiles/r04/r04ae_ab_c2_schedule.jsonl).
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
-    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes);  // hash_sched.hpp
+    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2);  // hash_sched.hpp
     const size_t njobs = sched.size();
     auto hasher = [&] {
         std::vector<spx::Blake2s> tmp(lanes);

@@ -3,9 +3,11 @@
 // runs it on threads and checks that every proof is absorbed exactly once for any pool size.
 //
 // Owned proofs are proved in waves of `wave` (the rank's share of one proof per context in flight:
-// ceil(nctx / G) when proof i is absorbed by rank i mod G). The first kScalarWaves waves
-// are absorbed one proof per job (scalar: ready after one absorption's time, as their proofs reach
-// their first challenge); every later proof in full-width multi-buffer jobs (`lanes` proofs each).
+// ceil(nctx / G) when proof i is absorbed by rank i mod G). The first `scalar_waves` waves (2 for
+// full proofs) are absorbed one proof per job (scalar: ready after one absorption's time, as their
+// proofs reach their first challenge); every later proof in full-width multi-buffer jobs (`lanes`
+// proofs each). With the commitment stubbed (BASELINE C2) a proof's device work is ~1% of one
+// absorption, so there is nothing to overlap and only the pool's throughput counts: 0 scalar waves.
 // The first kLead full-width jobs are claimed before the scalar ones, so they run from the start on
 // their own threads (kLead threads beyond the scalar part's) and are done before their waves start.
 #pragma once
@@ -18,14 +20,13 @@
 namespace spx {
 
 struct HashSched {
-    static constexpr int kScalarWaves = 2;
     static constexpr size_t kLead = 4;
     std::vector<std::pair<size_t, size_t>> jobs;  // [first, last) owned indices per job, in claim order
     size_t nlead = 0;                             // full-width jobs claimed ahead of the scalar ones
     std::atomic<size_t> next{0};
 
-    HashSched(size_t owned, size_t wave, int lanes) {
-        const size_t nscalar = lanes > 1 ? std::min(owned, (size_t)kScalarWaves * std::max<size_t>(wave, 1)) : owned;
+    HashSched(size_t owned, size_t wave, int lanes, int scalar_waves = 2) {
+        const size_t nscalar = lanes > 1 ? std::min(owned, (size_t)std::max(scalar_waves, 0) * std::max<size_t>(wave, 1)) : owned;
         std::vector<std::pair<size_t, size_t>> wide;
         for (size_t b = nscalar; b < owned; b += (size_t)lanes) wide.emplace_back(b, std::min(owned, b + (size_t)lanes));
         nlead = std::min(kLead, wide.size());

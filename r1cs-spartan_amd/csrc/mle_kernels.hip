@@ -228,8 +228,9 @@ __global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* 
 // lines are written by one CU); wave w takes slices w, w + 4, w + 8, w + 12, so the waves of a block get
 // similar totals. Lane l of a slice owns one column: its entries sit at off + 64 j + l (lane-contiguous
 // loads per step), and a lane idles only for the steps between its own length and the slice's longest.
-// The kernel is bound by the dependent multiply-accumulate chains of the Montgomery products (VALU
-// latency: two entries per step give each wave two independent chains), not by HBM.
+// Two Montgomery products per entry at the product's measured issue rate (~4 cycles per instruction)
+// put the floor near 72 us at 2^20, well above the 19 us of its HBM bytes; loading the
+// row words a step ahead measured no gain.
 __global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFactors ef, Fr* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const Fr* __restrict__ lo = ef.t[0];
@@ -618,12 +619,17 @@ DEV Fr shfl_fr(const Fr& a, int src) {
     return r;
 }
 DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// a wave's block of 64 * R chunks (global, contiguous) -> lane l's row l (R chunks)
+// a wave's block of 64 * R chunks (global, contiguous) -> registers, chunk 64 k + lane in t[k]
+// (lane-contiguous loads; split from the transposition so a kernel can issue the next table's loads
+// before it works on the current one)
 template <int R>
-DEV void wave_rows_in(const uint4* __restrict__ g, uint4* lds, uint4 (&row)[R], int lane) {
-    uint4 t[R];
+DEV void wave_load(const uint4* __restrict__ g, uint4 (&t)[R], int lane) {
 #pragma unroll
     for (int k = 0; k < R; ++k) t[k] = g[64 * k + lane];
+}
+// the loaded chunks -> lane l's row l (R chunks), through the wave's LDS region
+template <int R>
+DEV void wave_transpose(const uint4 (&t)[R], uint4* lds, uint4 (&row)[R], int lane) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int c = 64 * k + lane;
@@ -633,6 +639,13 @@ DEV void wave_rows_in(const uint4* __restrict__ g, uint4* lds, uint4 (&row)[R], 
 #pragma unroll
     for (int j = 0; j < R; ++j) row[j] = lds[lane * (R + 1) + j];
     wave_lds_sync();
+}
+// a wave's block of 64 * R chunks (global, contiguous) -> lane l's row l (R chunks)
+template <int R>
+DEV void wave_rows_in(const uint4* __restrict__ g, uint4* lds, uint4 (&row)[R], int lane) {
+    uint4 t[R];
+    wave_load<R>(g, t, lane);
+    wave_transpose<R>(t, lds, row, lane);
 }
 // lane l's row l (R chunks) -> the wave's block of 64 * R chunks (global, contiguous)
 template <int R>
@@ -659,10 +672,11 @@ DEV void fr_to(uint4& lo, uint4& hi, const Fr& a) {
 }
 // one table's 4 inputs of this lane's pair b -> (x0, x1) = (T[4b] + r (T[4b+1] - T[4b]), ...) and
 // the folded pair stored to out[2b], out[2b+1]; `base` = the wave's first pair
-DEV void wave_fold(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t base, const Fr& r, uint4* lds, int lane,
-                   Fr& x0, Fr& x1) {
+// the same from this table's chunks already loaded by wave_load<8>
+DEV void wave_fold_loaded(const uint4 (&raw)[8], Fr* __restrict__ out, uint64_t base, const Fr& r, uint4* lds, int lane,
+                          Fr& x0, Fr& x1) {
     uint4 a[8];
-    wave_rows_in<8>(reinterpret_cast<const uint4*>(in + 4 * base), lds, a, lane);
+    wave_transpose<8>(raw, lds, a, lane);
     const Fr a0 = fr_of(a[0], a[1]), a1 = fr_of(a[2], a[3]), a2 = fr_of(a[4], a[5]), a3 = fr_of(a[6], a[7]);
     Fr d0, d1;
     fe_sub(d0, a1, a0);
@@ -674,6 +688,12 @@ DEV void wave_fold(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t bas
     fr_to(o[0], o[1], x0);
     fr_to(o[2], o[3], x1);
     wave_rows_out<4>(reinterpret_cast<uint4*>(out + 2 * base), lds, o, lane);
+}
+DEV void wave_fold(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t base, const Fr& r, uint4* lds, int lane,
+                   Fr& x0, Fr& x1) {
+    uint4 raw[8];
+    wave_load<8>(reinterpret_cast<const uint4*>(in + 4 * base), raw, lane);
+    wave_fold_loaded(raw, out, base, r, lds, lane, x0, x1);
 }
 
 // this lane's pair of one table without a fold (round 1): (T[2b], T[2b+1])
@@ -701,19 +721,20 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, 
     for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < (half >> 6); w += waves) {
         const uint64_t base = w << 6;
         Fr x0[3], x1[3], e;
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            if constexpr (FOLD)
-                wave_fold(in.t[m], out.t[m], base, r, lds, lane, x0[m], x1[m]);
-            else
-                wave_pair(in.t[m], base, lds, lane, x0[m], x1[m]);
-        }
         if constexpr (FOLD) {
+            // one table at a time: the software-pipelined form (the next table's loads issued before
+            // the current one's fold) spills to 400 B of scratch per lane at 4 waves per SIMD and ran
+            // 81-86 us against 59-61 (profiles/r04/r04ab_ab_pipelined.jsonl); sumcheck 2 and the
+            // opening folds keep it (two tables / two halves: no extra spills)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) wave_fold(in.t[m], out.t[m], base, r, lds, lane, x0[m], x1[m]);
             uint4 ev[4];
             wave_rows_in<4>(reinterpret_cast<const uint4*>(Ein + 2 * base), lds, ev, lane);
             fe_add(e, fr_of(ev[0], ev[1]), fr_of(ev[2], ev[3]));
             if (Eout) st_fr(Eout + base + lane, e);
         } else {
+#pragma unroll
+            for (int m = 0; m < 3; ++m) wave_pair(in.t[m], base, lds, lane, x0[m], x1[m]);
             uint4 ev[2];
             wave_rows_in<2>(reinterpret_cast<const uint4*>(Ein + base), lds, ev, lane);
             e = fr_of(ev[0], ev[1]);
@@ -760,9 +781,12 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __
     for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < (half >> 6); w += waves) {
         const uint64_t base = w << 6;
         Fr m0, m1, z0, z1, t, u, v;
-        if constexpr (FOLD) {
-            wave_fold(Min, Mout, base, r, lds, lane, m0, m1);
-            wave_fold(Zin, Zout, base, r, lds, lane, z0, z1);
+        if constexpr (FOLD) {  // Z's loads in flight while M is folded
+            uint4 rm[8], rz[8];
+            wave_load<8>(reinterpret_cast<const uint4*>(Min + 4 * base), rm, lane);
+            wave_load<8>(reinterpret_cast<const uint4*>(Zin + 4 * base), rz, lane);
+            wave_fold_loaded(rm, Mout, base, r, lds, lane, m0, m1);
+            wave_fold_loaded(rz, Zout, base, r, lds, lane, z0, z1);
         } else {
             wave_pair(Min, base, lds, lane, m0, m1);
             wave_pair(Zin, base, lds, lane, z0, z1);
@@ -948,11 +972,15 @@ __global__ __launch_bounds__(kThreads) void k_open_fold_wave(const Fr* __restric
             wave_store_1(rout + base, u, lds, lane);
         } else {
             Fr q2 = {}, r = {};
+            // both halves' loads issued up front: the second half's are in flight during the first's work
+            uint4 raw0[8], raw1[8];
+            wave_load<8>(reinterpret_cast<const uint4*>(rin + 4 * (2 * base)), raw0, lane);
+            wave_load<8>(reinterpret_cast<const uint4*>(rin + 4 * (2 * base + 64)), raw1, lane);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const uint64_t grp = 2 * base + 64 * h;  // first group of this half (group = 4 entries)
                 uint4 in[8];
-                wave_rows_in<8>(reinterpret_cast<const uint4*>(rin + 4 * grp), lds, in, lane);
+                wave_transpose<8>(h ? raw1 : raw0, lds, in, lane);
                 Fr q0[2], q1, u, t;
                 fold_group4(in, fa, 0, q0, q1, u);
                 if (a.qoff[0] != ~0ull) wave_store_q(q, a.qoff[0], grp, q0, lds, lane);

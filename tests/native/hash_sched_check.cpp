@@ -1,6 +1,6 @@
 // spx_prove_many's hashing-pool plan (r1cs-spartan_amd/csrc/hash_sched.hpp) on real threads: for
 // every pool size, context count, lane width and proof count, each owned proof is absorbed by exactly
-// one job, the first two waves (2 nctx proofs) one per job, the lead full-width jobs first, and
+// one job, the first scalar waves (0, 1 or 2 waves of nctx proofs) one per job, the lead full-width jobs first, and
 // every thread terminates (a proof whose
 // job is never claimed would leave its prove waiting forever).
 #include <cstdio>
@@ -15,8 +15,8 @@ int main() {
         for (int nctx : {1, 4, 16, 64})
             for (int nh0 : {1, 2, 3, 4, 5, 8, 16, 32})
                 for (int lanes : {1, 8, 16})
-                    for (int rep = 0; rep < 3; ++rep) {
-                        spx::HashSched s(owned, (size_t)nctx, lanes);
+                    for (int sw : {0, 1, 2}) {
+                        spx::HashSched s(owned, (size_t)nctx, lanes, sw);
                         std::vector<std::atomic<int>> done(owned);
                         for (auto& d : done) d = 0;
                         const int nh = std::min<int>(nh0, (int)s.size());
@@ -34,7 +34,7 @@ int main() {
                                 return 1;
                             }
                         // claim order: the lead full-width jobs, the scalar jobs of the first two waves, the rest
-                        const size_t scalar = lanes > 1 ? std::min<size_t>(owned, 2 * nctx) : owned;
+                        const size_t scalar = lanes > 1 ? std::min<size_t>(owned, (size_t)sw * nctx) : owned;
                         for (size_t j = 0; j < s.size(); ++j) {
                             const size_t w = s.jobs[j].second - s.jobs[j].first;
                             const bool is_scalar = j >= s.nlead && j < s.nlead + scalar;

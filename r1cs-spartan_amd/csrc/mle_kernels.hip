@@ -724,8 +724,10 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, 
         if constexpr (FOLD) {
             // one table at a time: the software-pipelined form (the next table's loads issued before
             // the current one's fold) spills to 400 B of scratch per lane at 4 waves per SIMD and ran
-            // 81-86 us against 59-61 (profiles/r04/r04ab_ab_pipelined.jsonl); sumcheck 2 and the
-            // opening folds keep it (two tables / two halves: no extra spills)
+            // 81-86 us against 59-61 (profiles/r04/r04ab_ab_pipelined.jsonl); with the products taken as
+            // soon as their factors exist (only A B live) still 352 B and 73-74 us against 62-65
+            // (r04ag_ab_sc1_early_products.jsonl). Sumcheck 2 and the opening folds keep it (two tables
+            // / two halves: no extra spills)
 #pragma unroll
             for (int m = 0; m < 3; ++m) wave_fold(in.t[m], out.t[m], base, r, lds, lane, x0[m], x1[m]);
             uint4 ev[4];

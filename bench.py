@@ -834,6 +834,7 @@ def main():
                 "proofs_in_flight": len(hctxs),
                 "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
                 "comm": args.comm if sctxs else None,
+                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or None,  # hardware queues per process
             },
             "ms_per_proof_single": round(ms_1, 3),
             "value_single_proof": round(n / (ms_1 / 1e3), 1),

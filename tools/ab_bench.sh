@@ -7,8 +7,9 @@ set -e
 TAG="$1"; shift
 OUT="gpurun_out/$TAG.jsonl"
 : > "$OUT"
+read -r -a EXTRA <<< "${AB_ARGS:-}"  # split here, before any ALT changes IFS
 run() {  # $1 = label; remaining environment already exported by the caller
-  timeout -k 10 240 python bench.py --no-cpu --no-c2 --rehearse '' --steps 3 --warmup 1 ${AB_ARGS:-} \
+  timeout -k 10 240 python bench.py --no-cpu --no-c2 --rehearse '' --steps 3 --warmup 1 "${EXTRA[@]}" \
     | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(json.dumps({'build': '$1', 'value': d['value'], 'ms_single_cached': d['ms_per_proof_single_cached_transcript'], 'kernels': d['kernels_ms_per_proof'], 'hbm_largest': d['roofline'].get('hbm_kernels', {}).get('largest_launches'), 'host': d.get('host'), 'value_cached': d.get('value_index_cached_transcript')}))" >> "$OUT"
 }
 for i in 1 2; do

@@ -359,10 +359,11 @@ def largest_rate(d):
 
 
 def inflight_for(g):
-    """proofs in flight per rank for proofs sharded over g ranks (1: unsharded). Solo-rank sweeps on one
-    MI355X (profiles/r03/r03ak_inflight_hwq.jsonl, 32 hardware queues): 16 is best at g <= 2; a rank of
-    a 4- or 8-rank proof has 1/g of every kernel's work, so it needs 8 g proofs in flight to fill the GPU"""
-    return 16 if g <= 2 else min(64, 8 * g)
+    """proofs in flight per rank for proofs sharded over g ranks (1: unsharded). N = 1 with the round-4
+    hashing pool (16 hardware queues, profiles/r04/r04a[k-n]_ab_inflight.jsonl): 16 -> 61.0, 24 -> 62.2,
+    32 -> 62.8, 48 -> 62.9, 64 -> 62.7 M constraints/s (round 3 found 16 best while host hashing still
+    limited, r03ak); a rank of a 4- or 8-rank proof has 1/g of every kernel's work, so 8 g there"""
+    return 32 if g <= 2 else min(64, 8 * g)
 
 
 def hw_queues_for(g):

@@ -424,9 +424,18 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     // The first two waves are scalar; a few full-width jobs for the next waves start beside them. With
     // the commitment stubbed (C2), all full width: 277 -> 370 M constraints/s at 2^18 in the same A/B
     // (profiles/r04/r04ae_ab_c2_schedule.jsonl).
+    // Pool size: the hashers run ahead as fast as they can, so a pool larger than the cores it needs
+    // starves the proof threads of their host work (solo G = 8 rank, 64 in flight on 16 cores: 64
+    // hashers 332 M, 8 hashers 381 M constraints/s; profiles/r03/r03am_hash_threads.jsonl). A rank of a
+    // G-rank proof absorbs 1/G of the proofs: half the core budget for G >= 4, all of it otherwise.
+    // Budget: SPX_HASH_THREADS, else OMP_NUM_THREADS (the box's CPU share), else the hardware threads.
+    int budget = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("OMP_NUM_THREADS")) budget = atoi(e);
+    budget = std::max(1, budget);
+    const int nbase = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
-    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2);  // hash_sched.hpp
+    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2, 2 * (size_t)nbase);
     const size_t njobs = sched.size();
     auto hasher = [&] {
         std::vector<spx::Blake2s> tmp(lanes);
@@ -453,15 +462,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             cv.notify_all();
         }
     };
-    // Pool size: the hashers run ahead as fast as they can, so a pool larger than the cores it needs
-    // starves the proof threads of their host work (solo G = 8 rank, 64 in flight on 16 cores: 64
-    // hashers 332 M, 8 hashers 381 M constraints/s; profiles/r03/r03am_hash_threads.jsonl). A rank of a
-    // G-rank proof absorbs 1/G of the proofs: half the core budget for G >= 4, all of it otherwise.
-    // Budget: SPX_HASH_THREADS, else OMP_NUM_THREADS (the box's CPU share), else the hardware threads.
-    int budget = (int)std::thread::hardware_concurrency();
-    if (const char* e = getenv("OMP_NUM_THREADS")) budget = atoi(e);
-    budget = std::max(1, budget);
-    int nh = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget) + (int)sched.nlead;
+    int nh = nbase + (int)sched.nlead;
     if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
     nh = std::min<int>(nh, (int)njobs);
     std::vector<std::thread> pool;

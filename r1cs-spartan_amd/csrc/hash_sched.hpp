@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstddef>
+#include <cstdint>
 #include <utility>
 #include <vector>
 
@@ -25,8 +26,11 @@ struct HashSched {
     size_t nlead = 0;                             // full-width jobs claimed ahead of the scalar ones
     std::atomic<size_t> next{0};
 
-    HashSched(size_t owned, size_t wave, int lanes, int scalar_waves = 2) {
-        const size_t nscalar = lanes > 1 ? std::min(owned, (size_t)std::max(scalar_waves, 0) * std::max<size_t>(wave, 1)) : owned;
+    // max_scalar caps the scalar part (two rounds of the pool's threads: with many proofs in flight a
+    // wave is wider than the pool, and the full-width jobs beside it are ready as early)
+    HashSched(size_t owned, size_t wave, int lanes, int scalar_waves = 2, size_t max_scalar = SIZE_MAX) {
+        size_t nscalar = lanes > 1 ? std::min(owned, (size_t)std::max(scalar_waves, 0) * std::max<size_t>(wave, 1)) : owned;
+        if (lanes > 1) nscalar = std::min(nscalar, max_scalar);
         std::vector<std::pair<size_t, size_t>> wide;
         for (size_t b = nscalar; b < owned; b += (size_t)lanes) wide.emplace_back(b, std::min(owned, b + (size_t)lanes));
         nlead = std::min(kLead, wide.size());

@@ -3,6 +3,8 @@
 // one job, the first scalar waves (0, 1 or 2 waves of nctx proofs) one per job, the lead full-width jobs first, and
 // every thread terminates (a proof whose
 // job is never claimed would leave its prove waiting forever).
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <thread>
 #include <vector>
@@ -15,8 +17,9 @@ int main() {
         for (int nctx : {1, 4, 16, 64})
             for (int nh0 : {1, 2, 3, 4, 5, 8, 16, 32})
                 for (int lanes : {1, 8, 16})
-                    for (int sw : {0, 1, 2}) {
-                        spx::HashSched s(owned, (size_t)nctx, lanes, sw);
+                    for (int sw : {0, 1, 2})
+                    for (size_t cap : {(size_t)SIZE_MAX, (size_t)4, (size_t)32}) {
+                        spx::HashSched s(owned, (size_t)nctx, lanes, sw, cap);
                         std::vector<std::atomic<int>> done(owned);
                         for (auto& d : done) d = 0;
                         const int nh = std::min<int>(nh0, (int)s.size());
@@ -34,7 +37,7 @@ int main() {
                                 return 1;
                             }
                         // claim order: the lead full-width jobs, the scalar jobs of the first two waves, the rest
-                        const size_t scalar = lanes > 1 ? std::min<size_t>(owned, (size_t)sw * nctx) : owned;
+                        const size_t scalar = lanes > 1 ? std::min({(size_t)owned, (size_t)sw * nctx, cap}) : owned;
                         for (size_t j = 0; j < s.size(); ++j) {
                             const size_t w = s.jobs[j].second - s.jobs[j].first;
                             const bool is_scalar = j >= s.nlead && j < s.nlead + scalar;

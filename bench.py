@@ -358,6 +358,12 @@ def largest_rate(d):
     return {"MB": round(mb, 2), "us": round(us, 2), "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+# BASELINE C2 (commitment stubbed): 16 proofs in flight. Its proofs are ~100x shorter than a full
+# proof's absorption and its kernels small: with 32 contexts on 4 hardware queues the index-cached C2
+# rate fell 843 -> 446 M (profiles/r04/r04ao_bench.json against r04af_bench.json)
+C2_INFLIGHT = 16
+
+
 def inflight_for(g):
     """proofs in flight per rank for proofs sharded over g ranks (1: unsharded). N = 1 with the round-4
     hashing pool (16 hardware queues, profiles/r04/r04a[k-n]_ab_inflight.jsonl): 16 -> 61.0, 24 -> 62.2,
@@ -367,10 +373,12 @@ def inflight_for(g):
 
 
 def hw_queues_for(g):
-    """hardware queues per process (GPU_MAX_HW_QUEUES): 16 for up to 16 proofs in flight (32 measured
-    1% slower at N = 1, profiles/r03/r03al_ab_hwq.jsonl); 32 when 4- or 8-rank proofs keep 32-64 in flight
-    (profiles/r03/r03aj_g8_knobs.jsonl: 64 in flight on 32 queues +18% over 16 on 16)"""
-    return 16 if g <= 2 else 32
+    """hardware queues per process (GPU_MAX_HW_QUEUES): 4, HIP's default and the GPU box's preset, for
+    N <= 2 (round 4, 32 in flight: 4 -> 62.8 vs 32 -> 60.4 M, 24 in flight: 62.2 vs 60.9 M with 24 queues,
+    profiles/r04/r04a{i,j}_ab_inflight.jsonl; 8 queues no better, r04ah_ab_hwq8.jsonl); 32 when 4- or
+    8-rank proofs keep 32-64 in flight (profiles/r03/r03aj_g8_knobs.jsonl: 64 in flight on 32 queues
+    +18% over 16 on 16)"""
+    return 4 if g <= 2 else 32
 
 
 def lvl0_for(g):
@@ -544,10 +552,15 @@ def main():
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
     # hardware queues per process (HIP default 4): a proof's small latency-bound kernels (sumcheck
     # rounds, bucket-weighting levels) then queue behind fewer of the other proofs' MSM launches
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
+    # (set for G >= 4 even where the environment presets HIP's default 4; kept from the environment
+    # otherwise, so an A/B can vary it)
+    if world >= 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues_for(world))
+    else:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
     spx = load_product()
     L = spx.lib()
-    Bb = args.inflight or inflight_for(1)  # contexts of the unsharded (batch) proofs
+    Bb = args.inflight or (C2_INFLIGHT if stub else inflight_for(1))  # contexts of the unsharded (batch) proofs
     Bs = args.inflight or inflight_for(world)  # contexts of the proofs sharded over all ranks
     Bm = max(Bb, Bs, inflight_for(2))
     P = max(Bm, (args.proofs_per_step + Bm - 1) // Bm * Bm)  # proofs per step; each worker proves P / B of them
@@ -891,7 +904,7 @@ def main():
             rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
             out["proof_sharded_rehearsal"] = rehearsal
         if not stub and world == 1 and not args.no_c2:
-            out["c2"] = c2_line(spx, L, args, Bb)
+            out["c2"] = c2_line(spx, L, args, args.inflight or C2_INFLIGHT)
         return out
 
     out = make_out() if rank == 0 else None

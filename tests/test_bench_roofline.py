@@ -58,7 +58,7 @@ def test_settings_by_sharding_degree(bench):
     measured optima, every in-flight count divides the default 64 proofs per step, and the RCCL hub's
     64 channels cover the largest"""
     assert [bench.inflight_for(g) for g in (1, 2, 4, 8, 16)] == [32, 32, 32, 64, 64]
-    assert [bench.hw_queues_for(g) for g in (1, 2, 4, 8)] == [16, 16, 32, 32]
+    assert [bench.hw_queues_for(g) for g in (1, 2, 4, 8)] == [4, 4, 32, 32]
     assert [bench.lvl0_for(g) for g in (1, 2, 4, 8)] == [0, 0, 1, 1]
     for g in (1, 2, 4, 8):
         assert 64 % bench.inflight_for(g) == 0

@@ -128,6 +128,10 @@ int spx_ctx_set_lvl0_batch(spx_ctx *ctx, int mode);
  * recv receives world * bytes in rank order. For transport tests. */
 int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t bytes);
 
+/* free and total bytes of the context's device (hipMemGetInfo): bench.py sizes the proofs in flight
+ * per rank from it (each context keeps grow-only scratch and an MSM workspace) */
+int spx_ctx_mem_info(spx_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);
+
 /* ---- public parameters ---- */
 int spx_pp_load(spx_ctx *ctx, const uint8_t *bytes, size_t len, spx_pp **out);
 int spx_pp_generate(spx_ctx *ctx, int nv, uint64_t seed, spx_pp **out);
@@ -160,7 +164,10 @@ int spx_prove_many(spx_ctx **ctxs, int nctx, spx_pk *idx, spx_witness **wits, in
  * compressed as the reference's message types (ProverFirstMessage .. ProverSixthMessage, the
  * linear-sumcheck ProverMsg / IndexInfo). The session runs the same kernels as spx_prove: with the
  * challenges a Fiat-Shamir prove would draw, the messages concatenate to spx_prove's proof (plus the
- * two sumchecks' u64 round counts). One session or prove per context at a time.
+ * two sumchecks' u64 round counts). One session or prove per context at a time, enforced: from
+ * spx_prover_init until the session's last round (or spx_prover_free) the context is claimed, and a
+ * prove, verify, kernel-level call or second session on it fails with SPX_INVALID_ARGUMENT (so do
+ * two concurrent proves on one context). Sessions need an unsharded context (comm size 1).
  *   spx_prover_init                  prover_init              prover.rs:109-121 (|v| power of two, |v|+|w| = n)
  *   spx_prover_first_round           prover_first_round       prover.rs:123-141 (commitment)
  *   spx_prover_second_round          prover_second_round      prover.rs:143-160 (r_v: log2|v| coins)

@@ -93,6 +93,7 @@ EXPORTED = [
     "spx_comm_hub_destroy",
     "spx_ctx_comm_allgather",
     "spx_msm_reruns",
+    "spx_ctx_mem_info",
     "spx_pp_load",
     "spx_pp_generate",
     "spx_pp_serialize",
@@ -169,6 +170,8 @@ def lib():
         L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     if hasattr(L, "spx_msm_reruns") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_msm_reruns.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(L, "spx_ctx_mem_info") or not os.environ.get("SPX_LIB_PATH"):
+        L.spx_ctx_mem_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
         L.spx_ctx_set_lvl0_batch.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_comm_hub_create_rccl") or not os.environ.get("SPX_LIB_PATH"):  # A/B builds may predate the hub
@@ -338,6 +341,12 @@ class Context:
         out = ctypes.create_string_buffer(max(1, len(data) * world))
         _check(lib().spx_ctx_comm_allgather(self.h, data, out, len(data)))
         return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(world)]
+
+    def mem_info(self):
+        """(free, total) bytes of this context's device (spx_ctx_mem_info)"""
+        f, t = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().spx_ctx_mem_info(self.h, ctypes.byref(f), ctypes.byref(t)))
+        return f.value, t.value
 
     def msm_reruns(self):
         """MSM batches rerun with dense keys after a compacted-key overflow (spx_msm_reruns)"""
@@ -672,11 +681,16 @@ def sumcheck_round(ctx, f, g, r_prev=None):
     ([P(0), P(1), P(2)] as 32-byte strings, f', g') with f', g' the tables bound to r_prev (None in
     the first round)."""
     fb, gb = _as_bytes(f), _as_bytes(g)
+    # the native side reads 32 n bytes from both tables and 32 from r_prev: check before the call
+    if len(fb) != len(gb) or len(fb) % 32:
+        raise InvalidArgument("f and g must be equal-length tables of 32-byte field elements")
     n = len(fb) // 32
     ev = ctypes.create_string_buffer(96)
     fo = ctypes.create_string_buffer(max(16 * n, 1))
     go = ctypes.create_string_buffer(max(16 * n, 1))
     rb = None if r_prev is None else _as_bytes([r_prev] if isinstance(r_prev, int) else r_prev)
+    if rb is not None and len(rb) != 32:
+        raise InvalidArgument("r_prev must be one 32-byte field element")
     _check(lib().spx_sumcheck_round(ctx.h, fb, gb, n, rb, ev, fo, go))
     evals = [ev.raw[32 * k : 32 * k + 32] for k in range(3)]
     if r_prev is None:

@@ -328,6 +328,9 @@ int spx_prover_init(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, cons
         if (!idx || !out) spx::invalid("null prover key / out");
         if (!spx::is_pow2(nv)) spx::invalid("public input should be power of two");  // prover.rs:114-116
         if (nv + nw != idx->i->n) spx::invalid("|v| + |w| != number of variables");  // prover.rs:117-119
+        // a session freed mid-way cancels its worker at its next coin; on a sharded context the peer
+        // ranks would then wait in their next exchange with no error, so sessions are unsharded
+        if (ctx->c->comm->size() > 1) spx::invalid("round-level prover sessions need an unsharded context (comm size 1)");
         auto W = spx::witness_upload(*ctx->c, v, nv, w, nw);
         *out = new spx_prover{ctx, std::make_unique<spx::Interactive>(*ctx->c, *idx->i, std::move(W))};
     });
@@ -435,7 +438,12 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     const int nbase = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
-    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2, 2 * (size_t)nbase);
+    // SPX_HASH_THREADS replaces the pool size (lead jobs included) and with it the scalar cap
+    int nh_env = 0;
+    if (const char* e = getenv("SPX_HASH_THREADS")) nh_env = std::max(1, atoi(e));
+    const size_t nsize = nh_env ? (size_t)nh_env : (size_t)nbase + spx::HashSched::kLead;
+    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2,
+                         2 * (size_t)(nh_env ? nh_env : nbase), nsize);
     const size_t njobs = sched.size();
     auto hasher = [&] {
         std::vector<spx::Blake2s> tmp(lanes);
@@ -462,8 +470,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
             cv.notify_all();
         }
     };
-    int nh = nbase + (int)sched.nlead;
-    if (const char* e = getenv("SPX_HASH_THREADS")) nh = std::max(1, atoi(e));
+    int nh = nh_env ? nh_env : nbase + (int)sched.nlead;
     nh = std::min<int>(nh, (int)njobs);
     std::vector<std::thread> pool;
     for (int t = 0; t < nh; ++t) pool.emplace_back(hasher);
@@ -533,6 +540,7 @@ int spx_verify(spx_ctx* ctx, spx_pk* idx, const uint8_t* v, size_t nv, const uin
     return guard([&] {
         if (!idx || (nv && !v) || (len && !proof) || !vp) spx::invalid("null argument");
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         spx::verify(*ctx->c, *idx->i, v, nv, proof, len, spx::vp_load(vp, vp_len), opts_of(opts));
     });
 }
@@ -594,6 +602,16 @@ int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
         if (ops) *ops = ctx->c->kprof.ops[id];
     });
 }
+int spx_ctx_mem_info(spx_ctx* ctx, uint64_t* free_bytes, uint64_t* total_bytes) {
+    return guard([&] {
+        if (!free_bytes || !total_bytes) spx::invalid("null argument");
+        set_dev(ctx);
+        size_t f = 0, t = 0;
+        SPX_HIP(hipMemGetInfo(&f, &t));
+        *free_bytes = f;
+        *total_bytes = t;
+    });
+}
 int spx_msm_reruns(spx_ctx* ctx, uint64_t* reruns) {
     return guard([&] {
         if (!ctx || !reruns) spx::invalid("null argument");
@@ -603,6 +621,7 @@ int spx_msm_reruns(spx_ctx* ctx, uint64_t* reruns) {
 int spx_sum_over_y(spx_ctx* ctx, const spx_csr* m, const uint8_t* z, uint8_t* out) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_sum_over_y(*ctx->c, to_host(m), z);
         memcpy(out, r.data(), r.size());
     });
@@ -610,6 +629,7 @@ int spx_sum_over_y(spx_ctx* ctx, const spx_csr* m, const uint8_t* z, uint8_t* ou
 int spx_eval_on_x(spx_ctx* ctx, const spx_csr* m, const uint8_t* r_x, uint8_t* out) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_eval_on_x(*ctx->c, to_host(m), r_x);
         memcpy(out, r.data(), r.size());
     });
@@ -619,12 +639,14 @@ int spx_sumcheck_round(spx_ctx* ctx, const uint8_t* f, const uint8_t* g, size_t 
     return guard([&] {
         set_dev(ctx);
         if (!f || !g || !evals_out) spx::invalid("null argument");
+        spx::CtxClaim claim(*ctx->c);
         spx::k_sumcheck_round(*ctx->c, f, g, n, r_prev, evals_out, f_out, g_out);
     });
 }
 int spx_msm_g1(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out96) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_msm(*ctx->c, false, bases, scalars, n);
         memcpy(out96, r.data(), r.size());
     });
@@ -632,6 +654,7 @@ int spx_msm_g1(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_
 int spx_msm_g2(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_t n, uint8_t* out192) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_msm(*ctx->c, true, bases, scalars, n);
         memcpy(out192, r.data(), r.size());
     });
@@ -639,6 +662,7 @@ int spx_msm_g2(spx_ctx* ctx, const uint8_t* bases, const uint8_t* scalars, size_
 int spx_commit(spx_ctx* ctx, spx_pp* pp, const uint8_t* table, int nv, uint8_t* out56) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_commit(*ctx->c, *pp->p, table, nv);
         memcpy(out56, r.data(), r.size());
     });
@@ -647,6 +671,7 @@ int spx_open(spx_ctx* ctx, spx_pp* pp, const uint8_t* table, int nv, const uint8
              uint8_t* proof_out) {
     return guard([&] {
         set_dev(ctx);
+        spx::CtxClaim claim(*ctx->c);
         auto r = spx::k_open(*ctx->c, *pp->p, table, nv, point);
         memcpy(eval_out, r.data(), 32);
         memcpy(proof_out, r.data() + 32, r.size() - 32);

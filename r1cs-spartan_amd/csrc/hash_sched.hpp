@@ -10,6 +10,9 @@
 // absorption, so there is nothing to overlap and only the pool's throughput counts: 0 scalar waves.
 // The first kLead full-width jobs are claimed before the scalar ones, so they run from the start on
 // their own threads (kLead threads beyond the scalar part's) and are done before their waves start.
+// With a pool of `threads` threads at most threads - 1 jobs lead, so at least one thread starts on the
+// scalar jobs of the first wave (a pool of 1 or 2 threads would otherwise spend its first ~0.3 s on
+// later waves' full-width jobs while the first proofs wait).
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -28,12 +31,14 @@ struct HashSched {
 
     // max_scalar caps the scalar part (two rounds of the pool's threads: with many proofs in flight a
     // wave is wider than the pool, and the full-width jobs beside it are ready as early)
-    HashSched(size_t owned, size_t wave, int lanes, int scalar_waves = 2, size_t max_scalar = SIZE_MAX) {
+    HashSched(size_t owned, size_t wave, int lanes, int scalar_waves = 2, size_t max_scalar = SIZE_MAX,
+              size_t threads = SIZE_MAX) {
         size_t nscalar = lanes > 1 ? std::min(owned, (size_t)std::max(scalar_waves, 0) * std::max<size_t>(wave, 1)) : owned;
         if (lanes > 1) nscalar = std::min(nscalar, max_scalar);
         std::vector<std::pair<size_t, size_t>> wide;
         for (size_t b = nscalar; b < owned; b += (size_t)lanes) wide.emplace_back(b, std::min(owned, b + (size_t)lanes));
         nlead = std::min(kLead, wide.size());
+        if (nscalar > 0) nlead = std::min(nlead, threads > 0 ? threads - 1 : 0);
         jobs.assign(wide.begin(), wide.begin() + nlead);
         for (size_t b = 0; b < nscalar; ++b) jobs.emplace_back(b, b + 1);
         jobs.insert(jobs.end(), wide.begin() + nlead, wide.end());

@@ -36,7 +36,9 @@ struct Interactive::Coins : ExternalCoins {
     }
 };
 
-Interactive::Interactive(Ctx& c, Index& i, std::unique_ptr<Witness> w) : C(c), I(i), W(std::move(w)) {}
+// The session claims its context from prover_init until its worker's prove() has returned (or the
+// session is freed): a prove, verify or second session on the same context is refused meanwhile.
+Interactive::Interactive(Ctx& c, Index& i, std::unique_ptr<Witness> w) : C(c), I(i), W(std::move(w)) { claim.take(C); }
 
 Interactive::~Interactive() {
     {
@@ -44,7 +46,8 @@ Interactive::~Interactive() {
         cancel = true;
     }
     cv.notify_all();
-    if (th.joinable()) th.join();
+    if (th.joinable()) th.join();  // the unwinding prove drained both streams (UnwindDrain)
+    claim.release();
 }
 
 void Interactive::start(PP* P) {
@@ -58,12 +61,14 @@ void Interactive::start(PP* P) {
             SPX_HIP(hipSetDevice(dev));
             ProveOpts o;
             o.coins = coins_.get();
+            o.claimed = true;
             proof = prove(C, I, *W, pp, o);
         } catch (const Cancelled&) {
         } catch (...) {
             e = std::current_exception();
         }
         std::lock_guard<std::mutex> lk(mu);
+        claim.release();  // prove() has returned: its streams are idle
         err = e;
         final_proof = std::move(proof);
         finished = true;
@@ -137,8 +142,9 @@ std::vector<uint8_t> Interactive::sumcheck_round(int which, const uint8_t* ch) {
 // prove_fourth_round (prover.rs:210-228): the last point of r_x -> va, vb, vc
 std::vector<uint8_t> Interactive::fourth_round(const uint8_t* last) {
     if (next != kSumcheck1 || rounds != I.log_n) invalid("prove_fourth_round before the first sumcheck's last round");
+    auto c = coins_of(last, 1);  // a non-canonical coin leaves the session where it was (retry allowed)
     next = kFourth;
-    auto m = step(kFourth, coins_of(last, 1), 1);
+    auto m = step(kFourth, c, 1);
     next = kFifth;
     return m;
 }

@@ -45,6 +45,7 @@ struct Interactive {
     std::vector<uint8_t> final_proof;
     std::unique_ptr<Coins> coins_;
     std::thread th;
+    CtxClaim claim;  // held from construction until the worker's prove() returns
 };
 
 }  // namespace spx

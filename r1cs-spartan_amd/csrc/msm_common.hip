@@ -65,13 +65,16 @@ DEV uint32_t digit_ref(const MsmInst& I, uint32_t w, uint64_t j, int32_t d) {
 // One thread per scalar. Dense: a (key, reference) pair for every (scalar, window), window-major
 // within each instance so the stores coalesce; digits that are zero or not this rank's get the key
 // nb and sort last. Compact (proof-sharded ranks): only this rank's digits, appended through a
-// block-level scan and one atomic per block (st[1]); pairs past `cap` are dropped and flag st[0];
-// the last block to finish (ticket st[2]) fills the unused key slots with ~0 (sorts last).
-template <bool COMPACT>
+// block-level scan and one atomic per block (st[1]); pairs past `cap` are dropped and flag st[0].
+// Compact with HIST (the counting sort): each kept digit also takes its rank inside its bucket from
+// the bucket's counter (hist[key]++, returned into posv); otherwise the last block to finish (ticket
+// st[2]) fills the unused key slots with ~0 (sorts last in the radix sort).
+template <bool COMPACT, bool HIST>
 __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
                                                      int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t cap,
-                                                     uint32_t* __restrict__ st) {
+                                                     uint32_t* __restrict__ st, uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ posv) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = g < total;
     if (!COMPACT && !live) return;
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
         // counting pass keeps every window's key and reference in registers (the window loop unrolled,
         // so the arrays are indexed statically); more windows recompute them in the writing pass
         constexpr uint32_t kKeep = 16;
-        uint32_t cnt = 0, kkey[kKeep], kref[kKeep];
+        uint32_t cnt = 0, kkey[kKeep], kref[kKeep], kpos[kKeep];
         if (live && I.W <= kKeep) {
             Digits d = d0;
 #pragma unroll
@@ -113,6 +116,8 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                     kref[w] = digit_ref(I, w, j, dg);
                 }
                 cnt += kkey[w] != ~0u;
+                // independent returning atomics, issued back to back (their latency overlaps)
+                if constexpr (HIST) kpos[w] = kkey[w] != ~0u ? atomicAdd(&hist[kkey[w]], 1u) : 0u;
             }
         } else if (live) {
             Digits d = d0;
@@ -137,6 +142,7 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                     if (pos < cap) {
                         keys[pos] = kkey[w];
                         vals[pos] = kref[w];
+                        if constexpr (HIST) posv[pos] = kpos[w];
                     }
                     ++pos;
                 }
@@ -147,13 +153,16 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                 const int32_t dg = d.next(I.c);
                 const uint32_t key = digit_key(I, dg);
                 if (key == ~0u) continue;
+                const uint32_t rk = HIST ? atomicAdd(&hist[key], 1u) : 0u;
                 if (pos < cap) {
                     keys[pos] = key;
                     vals[pos] = digit_ref(I, w, j, dg);
+                    if constexpr (HIST) posv[pos] = rk;
                 }
                 ++pos;
             }
         }
+        if constexpr (HIST) return;  // the counting sort places the pairs itself: no fillers
         if (threadIdx.x == 0)  // (its cursor add has returned: every block's slots are taken when the last ticket is)
             last = atomicAdd(&st[2], 1u) == gridDim.x - 1;
         __syncthreads();
@@ -162,6 +171,81 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
             for (uint32_t i = used + threadIdx.x; i < cap; i += blockDim.x) keys[i] = ~0u;
         }
     }
+}
+
+// ------------------------------------------------------------------ counting sort (compacted batches)
+// A proof-sharded rank keeps 1/G of the digits (G = 8 at 2^20: ~2 M pairs per batch into 2^12..2^16
+// local buckets). Their order is: keys pass (hist[key]++ gives each pair its rank in its bucket) ->
+// ONE workgroup derives every offset array from the counts -> one scatter pass. Three launches, no
+// device-wide look-back scans, no fill kernels; the radix sort stays for dense batches.
+static constexpr int kScanThreads = 1024;
+static constexpr int kMaxLev = 8;
+struct LevPtrs {
+    uint32_t* p[kMaxLev + 1];  // [0]: the affine level's partial offsets; [l]: XYZZ level l
+};
+// exclusive scan of value(b), b = 0..n-1, over one workgroup (each thread a contiguous chunk); writes
+// out[b] (0 everywhere when `zero`); returns the total (every thread). Ends with a barrier, so `out`
+// is visible to the whole workgroup afterwards.
+template <class V>
+DEV uint32_t wg_scan(uint32_t n, V value, uint32_t* __restrict__ out, bool zero) {
+    using Scan = hipcub::BlockScan<uint32_t, kScanThreads>;
+    __shared__ typename Scan::TempStorage tmp;
+    const uint32_t E = (n + kScanThreads - 1) / kScanThreads;
+    const uint32_t b0 = min(n, threadIdx.x * E), b1 = min(n, b0 + E);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += value(b);
+    uint32_t pre, agg;
+    Scan(tmp).ExclusiveSum(sum, pre, agg);
+    for (uint32_t b = b0; b < b1; ++b) {
+        out[b] = zero ? 0u : pre;
+        pre += value(b);
+    }
+    __syncthreads();
+    return agg;
+}
+// hist (nb counts) -> offs (nb + 1), lev.p[0] (partials of seg1-reference thread ranges) and
+// lev.p[1..nlev] (segments of kSeg partials), exactly the arrays scan_partials / scan_segs give the
+// dense path; hist is cleared for the next batch. If the counted pairs exceed the capacity (the
+// compaction dropped some), the batch is flagged kMsmOverflow and every offset is 0: later kernels see
+// empty buckets, never read an unwritten slot, and the driver reruns the batch dense.
+__global__ __launch_bounds__(kScanThreads) void k_msm_offsets(uint32_t* __restrict__ hist, uint32_t nb, uint32_t cap,
+                                                              uint32_t* __restrict__ st, uint32_t* __restrict__ offs,
+                                                              uint32_t seg1, int nlev, LevPtrs lev) {
+    __shared__ uint32_t s_total;
+    {  // pass 1: the total, to decide overflow before anything is written
+        using Red = hipcub::BlockReduce<uint32_t, kScanThreads>;
+        __shared__ typename Red::TempStorage rt;
+        uint32_t sum = 0;
+        for (uint32_t b = threadIdx.x; b < nb; b += kScanThreads) sum += hist[b];
+        const uint32_t t = Red(rt).Sum(sum);
+        if (threadIdx.x == 0) s_total = t;
+        __syncthreads();
+    }
+    const bool over = s_total > cap;
+    if (over && threadIdx.x == 0) atomicOr(&st[0], kMsmOverflow);
+    wg_scan(nb + 1, [&](uint32_t b) { return b < nb ? hist[b] : 0u; }, offs, over);
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanThreads) hist[b] = 0u;
+    const uint32_t* prev = offs;
+    wg_scan(nb + 1, [&](uint32_t b) -> uint32_t {
+        if (b >= nb) return 0u;
+        const uint32_t o = prev[b], c = prev[b + 1] - o;
+        return c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0u;
+    }, lev.p[0], over);
+    for (int l = 1; l <= nlev; ++l) {
+        const uint32_t* pv = lev.p[l - 1];
+        wg_scan(nb + 1, [&](uint32_t b) -> uint32_t { return b < nb ? (pv[b + 1] - pv[b] + kSeg - 1) / kSeg : 0u; },
+                lev.p[l], over);
+    }
+}
+// compacted pair i -> refs[offs[key] + its rank in the bucket] (skipped when the batch overflowed)
+__global__ __launch_bounds__(kLight) void k_msm_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ posv, const uint32_t* __restrict__ st,
+                                                        uint32_t cap, const uint32_t* __restrict__ offs,
+                                                        uint32_t* __restrict__ refs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (st[0] & kMsmOverflow) return;
+    if (i >= min(st[1], cap)) return;
+    refs[offs[keys[i]] + posv[i]] = vals[i];
 }
 
 // sorted keys -> offs[b] = first index with key >= b, for b = 0..nb (offs[nb] = the references;
@@ -358,13 +442,40 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
     p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
 }
 
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s) {
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s, uint32_t seg1,
+                   int nlev) {
     MsmSorted o;
     const uint32_t nb = p.nb;
     const uint64_t n = p.tot_refs;
     const int nact = (int)p.insts.size();
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
     o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(n, 1));
+    if (p.compact) {  // counting sort: keys + counts, every offset array in one workgroup, scatter
+        if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
+        uint32_t* hist = (uint32_t*)ws->hist.ensure(4 * (size_t)std::max<uint32_t>(nb, 1));
+        if (ws->hist_zeroed != ws->hist.cap) {  // fresh allocation: zero once; the offsets kernel keeps it zero
+            HIPCHK(hipMemsetAsync(hist, 0, ws->hist.cap, s));
+            ws->hist_zeroed = ws->hist.cap;
+        }
+        uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * std::max<uint64_t>(n, 1));
+        uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
+        uint32_t* pv = (uint32_t*)ws->posv.ensure(4 * std::max<uint64_t>(n, 1));
+        uint32_t* lv = (uint32_t*)ws->lvl.ensure(4 * (size_t)(nb + 1) * (nlev + 1));
+        LevPtrs lp{};
+        for (int l = 0; l <= nlev; ++l) lp.p[l] = lv + (size_t)l * (nb + 1);
+        const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
+        kp_begin(KP_SORT, s);
+        hipLaunchKernelGGL((k_msm_keys<true, true>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
+                           scalars, ka, va, (uint32_t)n, st, hist, pv);
+        hipLaunchKernelGGL(k_msm_offsets, dim3(1), dim3(kScanThreads), 0, s, hist, nb, (uint32_t)n, st, o.offs, seg1, nlev,
+                           lp);
+        hipLaunchKernelGGL(k_msm_scatter, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, ka, va, pv, st,
+                           (uint32_t)n, o.offs, o.refs);
+        kp_end(32.0 * p.tot_sc + 4.0 * 6 * n, s);
+        o.np_off = lp.p[0];
+        for (int l = 1; l <= nlev; ++l) o.lev.push_back(lp.p[l]);
+        return o;
+    }
     // (bucket, reference) pairs, LSD radix sort on the bucket bits, bucket bounds by binary search
     int bits = 1;
     while ((1ull << bits) <= nb) ++bits;  // keys 0..nb; the compact filler ~0 has all these bits set
@@ -375,12 +486,8 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     // (a counting sort, histogram atomics in the keys pass + scan + scatter, measured 10% slower end to
     // end: profiles/r03/r03t_ab.jsonl; 11-bit onesweep digits no faster: r03at_ab_sort_bits.jsonl)
     kp_begin(KP_SORT, s);
-    if (p.compact)
-        hipLaunchKernelGGL(k_msm_keys<true>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, (uint32_t)n, st);
-    else
-        hipLaunchKernelGGL(k_msm_keys<false>, dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, 0u, st);
+    hipLaunchKernelGGL((k_msm_keys<false, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
+                       nb, scalars, ka, va, 0u, st, nullptr, nullptr);
     {
         hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
         size_t tb = 0;

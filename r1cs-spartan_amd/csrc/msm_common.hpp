@@ -108,6 +108,11 @@ struct PinArena {
 
 struct MsmWorkspace {
     DBuf tables, offs, refs, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a;
+    // compacted (proof-sharded) batches: per-bucket counts (all zero between batches: the offsets
+    // kernel clears what the keys kernel counted), each digit's rank inside its bucket, and the
+    // offset arrays of the affine level and of every XYZZ partial level
+    DBuf hist, posv, lvl;
+    size_t hist_zeroed = 0;  // bytes of `hist` known to be zero
     // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
     // rank's buckets (e.g. many equal values) stops overflowing after its first batch
     double cap_scale = 1.0;
@@ -144,8 +149,16 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s);
 // Digit / sort stage: sorted (bucket, reference) pairs, per-bucket offsets (offs[nb] = references).
 struct MsmSorted {
     uint32_t *offs, *refs;
+    // compacted batches (counting sort): the partial offsets of the affine level (seg1) and of each
+    // planned XYZZ level, computed in the same launch as offs; null / empty for dense batches, whose
+    // offsets come from scan_partials / scan_segs
+    uint32_t* np_off = nullptr;
+    std::vector<uint32_t*> lev;
 };
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* status_words, hipStream_t s);
+// seg1 / nlev: the affine level's references per thread and the number of XYZZ partial levels the
+// driver will run (used by the compacted path, which derives every level's offsets in one launch)
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* status_words, hipStream_t s,
+                   uint32_t seg1, int nlev);
 // exclusive offsets of the load-balanced affine level's partials per bucket (the seg-length thread
 // ranges a bucket's references [offs[b], offs[b + 1]) meet); np_off[nb] = all partials
 void scan_partials(MsmWorkspace* ws, const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np_off, hipStream_t s);

@@ -540,17 +540,28 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     const int nact = (int)pl.insts.size();
     if (!nact) return;
     msm_upload_plan(ws, pl, s);
-    MsmSorted so = msm_sort(ws, pl, scalars, st, s);
     const uint32_t nb = pl.nb;
     const uint64_t tot_refs = pl.tot_refs;
     // level 1: affine references -> XYZZ partials, one per segment of kSeg1 references
     const uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
+    // XYZZ partial levels, planned from the expected occupancy (no host round trip): a bucket with
+    // mu references on average rarely exceeds mu + 6 sqrt(mu) + 16; the weighting leaf adds the
+    // partials of any bucket that does (k_tree_chunk), so the plan decides speed, never correctness
+    const double mu = pl.mu_max;
+    int nlev = 0;
+    for (uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1; m > 1; m = (m + kSeg - 1) / kSeg)
+        ++nlev;  // partials per bucket, divided by kSeg per level
+    MsmSorted so = msm_sort(ws, pl, scalars, st, s, kSeg1, nlev);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
-    uint32_t* cur_off = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
-    uint32_t* nxt_off = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
-    scan_partials(ws, so.offs, nb, kSeg1, cur_off, s);
+    uint32_t* cur_off = so.np_off;
+    uint32_t* nxt_off = nullptr;
+    if (!cur_off) {  // dense batch: device-wide scans
+        cur_off = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
+        nxt_off = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
+        scan_partials(ws, so.offs, nb, kSeg1, cur_off, s);
+    }
     const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, cur_off, so.refs, pts, PA,
@@ -561,13 +572,11 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     Xyzz<F>* cur = PA;
     Xyzz<F>* nxt = PB;
     uint64_t cur_max_segs = max_segs;
-    // XYZZ partial levels, planned from the expected occupancy (no host round trip): a bucket with
-    // mu references on average rarely exceeds mu + 6 sqrt(mu) + 16; the weighting leaf adds the
-    // partials of any bucket that does (k_tree_chunk), so the plan decides speed, never correctness
-    const double mu = pl.mu_max;
-    uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1;  // partials per bucket
-    while (m > 1) {
-        scan_segs(ws, cur_off, nb, kSeg, nxt_off, s);
+    for (int l = 0; l < nlev; ++l) {
+        if (so.np_off)
+            nxt_off = so.lev[l];  // computed with the bucket offsets (counting sort)
+        else
+            scan_segs(ws, cur_off, nb, kSeg, nxt_off, s);
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
         hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur, nxt);
@@ -575,7 +584,6 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
         std::swap(cur, nxt);
         std::swap(cur_off, nxt_off);
         cur_max_segs = nsegs;
-        m = (m + kSeg - 1) / kSeg;
     }
     // bucket weighting tree over each instance's 2^lb local buckets: leaf, middle levels, top
     uint32_t tot_nodes = 0;

@@ -1025,6 +1025,8 @@ static HFr quad_at(const HFr g[3], const HFr& t) {
 
 // ====================================================================== prove
 std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts& o) {
+    CtxClaim claim;
+    if (!o.claimed) claim.take(C);  // before anything is queued: a refused prove touches nothing
     // A prove that throws may leave work queued on both streams that still reads W.z and writes the
     // context's slots: drain them while unwinding, so the caller may free the witness and the next
     // proof on this context starts from idle streams.

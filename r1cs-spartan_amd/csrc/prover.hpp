@@ -190,6 +190,9 @@ struct Ctx {
     int lvl0_mode = -1;         // shared level-0 opening MSM: 1 inside the first opening's batch, 0 beside
                                 // the commitment, -1 the process default (SPX_LVL0=batch -> 1)
     std::atomic<uint64_t> msm_reruns{0};  // MSM batches rerun dense after a compacted-key overflow
+    // one prove or round-level session at a time: both own the streams, the scratch tables, the pinned
+    // carve-out and the sumcheck ticket (CtxClaim)
+    std::atomic<bool> in_use{false};
     Ctx(int dev);
     ~Ctx();
     // region [off, off + bytes) of the pinned carve-out (throws if it does not fit its region)
@@ -203,6 +206,27 @@ struct Ctx {
         if (!side) return;
         SPX_HIP(hipStreamSynchronize(side));
         msm_ws_staging_reset(msm_side);
+    }
+};
+
+// Claims a context for one prove or one round-level session; a second claim while one is held fails
+// with SPX_INVALID_ARGUMENT instead of overwriting the holder's device tables.
+struct CtxClaim {
+    Ctx* c = nullptr;
+    CtxClaim() = default;
+    explicit CtxClaim(Ctx& C) { take(C); }
+    CtxClaim(const CtxClaim&) = delete;
+    CtxClaim& operator=(const CtxClaim&) = delete;
+    ~CtxClaim() { release(); }
+    void take(Ctx& C) {
+        bool want = false;
+        if (!C.in_use.compare_exchange_strong(want, true))
+            throw SpxError(kInvalidArgument, "context is in use by another prove or round-level prover session");
+        c = &C;
+    }
+    void release() {
+        if (c) c->in_use.store(false);
+        c = nullptr;
     }
 };
 
@@ -295,6 +319,7 @@ struct ProveOpts {
     // interactive prove (round-level API, interactive.cpp): messages out, verifier coins in; no
     // Fiat-Shamir absorption at all
     ExternalCoins* coins = nullptr;
+    bool claimed = false;  // the caller already holds the context's CtxClaim (a round-level session)
 };
 // Blake2s state after absorbing A, B, C (lib.rs:61-64): the per-proof sequential host work
 Blake2s absorb_matrices(const Index& I);

@@ -19,7 +19,7 @@ int main() {
                 for (int lanes : {1, 8, 16})
                     for (int sw : {0, 1, 2})
                     for (size_t cap : {(size_t)SIZE_MAX, (size_t)4, (size_t)32}) {
-                        spx::HashSched s(owned, (size_t)nctx, lanes, sw, cap);
+                        spx::HashSched s(owned, (size_t)nctx, lanes, sw, cap, (size_t)nh0);
                         std::vector<std::atomic<int>> done(owned);
                         for (auto& d : done) d = 0;
                         const int nh = std::min<int>(nh0, (int)s.size());
@@ -38,6 +38,12 @@ int main() {
                             }
                         // claim order: the lead full-width jobs, the scalar jobs of the first two waves, the rest
                         const size_t scalar = lanes > 1 ? std::min({(size_t)owned, (size_t)sw * nctx, cap}) : owned;
+                        // a pool of nh0 threads leads with at most nh0 - 1 full-width jobs when there are
+                        // scalar jobs, so one thread starts on the first wave
+                        if (scalar > 0 && s.nlead + 1 > (size_t)nh0) {
+                            printf("FAIL owned %d nctx %d threads %d: %zu lead jobs\n", owned, nctx, nh0, s.nlead);
+                            return 1;
+                        }
                         for (size_t j = 0; j < s.size(); ++j) {
                             const size_t w = s.jobs[j].second - s.jobs[j].first;
                             const bool is_scalar = j >= s.nlead && j < s.nlead + scalar;

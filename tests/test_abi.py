@@ -85,3 +85,14 @@ def test_no_cpu_fallback_without_gpu(spx):
         pytest.skip("a GPU is present")
     with pytest.raises(spx.SpartanError):
         spx.Context(0)
+
+
+def test_sumcheck_round_argument_checks(spx):
+    """spx.sumcheck_round checks its buffers before the native call, which reads 32 n bytes of both
+    tables and 32 bytes of r_prev (no context is touched: these fail on any machine)"""
+    with pytest.raises(spx.InvalidArgument):  # g shorter than f
+        spx.sumcheck_round(None, [1, 2, 3, 4], [1, 2, 3])
+    with pytest.raises(spx.InvalidArgument):  # not a whole number of 32-byte elements
+        spx.sumcheck_round(None, b"\x01" * 100, b"\x01" * 100)
+    with pytest.raises(spx.InvalidArgument):  # r_prev of the wrong size
+        spx.sumcheck_round(None, [1, 2, 3, 4], [1, 2, 3, 4], b"\x01" * 16)

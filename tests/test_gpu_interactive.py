@@ -128,6 +128,47 @@ def test_interactive_errors(spx, ctx, oc):
     assert pm6 == _oracle_run(oc, inst, ppc, 1234)[1]
 
 
+def test_interactive_claims_context_and_fourth_round_retry(spx, ctx, oc):
+    """a session owns its context's streams and tables until its worker's prove() returns: a prove, a
+    verify or a second session on that context is refused (SPX_INVALID_ARGUMENT) instead of
+    overwriting them; a non-canonical coin in the fourth round leaves the session retryable"""
+    log_n, log_v = 6, 2
+    inst = oc.Instance(0, log_n, log_v, 41)
+    pp = spx.MLProofForR1CS.setup(ctx, log_n, 43)
+    ppc = oc.PP.load(pp.serialize_uncompressed())
+    pk = spx.MLArgumentForR1CS.index(ctx, *[spx.Csr(M.n, M.row_ptr, M.col, M.val) for M in inst.mats])
+    seed = 4242
+    coins = Coins(seed)
+    p = spx.InteractiveProver(pk, inst.v_bytes, inst.w_bytes)
+    with pytest.raises(spx.InvalidArgument):  # the context is claimed from prover_init on
+        spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+    with pytest.raises(spx.InvalidArgument):
+        spx.InteractiveProver(pk, inst.v_bytes, inst.w_bytes)
+    msgs = [p.prover_first_round(pp), p.prover_second_round(coins.take(log_v), pp),
+            p.prover_third_round(coins.take(log_n))]
+    with pytest.raises(spx.InvalidArgument):  # mid-session: the worker holds the tables
+        spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+    ch = None
+    for _ in range(log_n):
+        msgs.append(p.prove_first_sumcheck_round(ch))
+        ch = coins.rand_fr()
+    with pytest.raises(spx.SerializationError):  # non-canonical last point of r_x
+        p.prove_fourth_round(R.to_bytes(32, "little"))
+    msgs.append(p.prove_fourth_round(ch))  # the retry is accepted
+    msgs.append(p.prove_fifth_round(*coins.take(3)))
+    ch = None
+    for _ in range(log_n):
+        msgs.append(p.prove_second_sumcheck_round(ch))
+        ch = coins.rand_fr()
+    pm6 = p.prove_sixth_round(ch, pp)
+    want_msgs, want_pm6, _ = _oracle_run(oc, inst, ppc, seed)
+    assert msgs == want_msgs and pm6 == want_pm6
+    # the worker has finished: the context is free again while the session object still exists
+    proof = spx.MLArgumentForR1CS.prove(pk, inst.v_bytes, inst.w_bytes, pp)
+    assert proof == oc.prove(inst.mats, inst.v_bytes, inst.w_bytes, ppc, 0, 0)
+    p.close()
+
+
 @pytest.mark.parametrize("log_n", [1, 2, 6, 13])
 def test_sumcheck_round_entry(spx, ctx, log_n):
     import spartan

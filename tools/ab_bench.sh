@@ -1,7 +1,7 @@
 # A/B of library builds / environment settings on one box (run via gpurun from the repo root):
 #   tools/ab_bench.sh TAG ALT1 [ALT2 ...]
 # Each ALT is an alternative .so (used through SPX_LIB_PATH) or VAR=value settings joined by ','
-# (e.g. SPX_WINDOW_BITS_LARGE=18). AB_ARGS adds bench.py arguments to every run (e.g. --config c2). Rounds alternate the default and every alternative, twice, with a
+# (e.g. SPX_HASH_THREADS=8,SPX_LVL0=batch). AB_ARGS adds bench.py arguments to every run (e.g. --config c2). Rounds alternate the default and every alternative, twice, with a
 # short bench (no CPU baseline, no C2 line); one JSON line per run into gpurun_out/<TAG>.jsonl.
 set -e
 TAG="$1"; shift

@@ -381,6 +381,27 @@ def hw_queues_for(g):
     return 4 if g <= 2 else 32
 
 
+# device memory kept free beyond the contexts' own footprint (HIP runtime, fragmentation, the
+# index-cached runs' second-stream MSM workspace, per-launch temporaries)
+FIT_RESERVE = 8 << 30
+
+
+def fit_inflight(ctxs, probe, reserve=FIT_RESERVE):
+    """how many of `ctxs` fit the device: probe() runs one proof on ctxs[0] (its grow-only scratch,
+    slots and MSM workspace reach their steady size, as every context's first proof makes them);
+    per-context bytes = the drop in free device memory. Returns (count, record). At 2^20 nothing
+    binds (~1.4 GiB per context); at 2^24 a context takes ~3 GiB beside ~90 GiB of PP, so a rank's
+    64 in flight would not fit."""
+    f0, total = ctxs[0].mem_info()
+    probe()
+    f1, _ = ctxs[0].mem_info()
+    per = max(f0 - f1, 1)
+    fit = int(min(len(ctxs), 1 + max(0, (f1 - reserve) // per)))
+    return fit, {"free_before_GiB": round(f0 / 2**30, 2), "free_after_one_GiB": round(f1 / 2**30, 2),
+                 "per_context_GiB": round(per / 2**30, 3), "total_GiB": round(total / 2**30, 2),
+                 "reserve_GiB": round(reserve / 2**30, 2), "contexts": fit, "wanted": len(ctxs)}
+
+
 def lvl0_for(g):
     """level-0 opening MSM inside the first opening's batch (one MSM pipeline less per proof) for proofs
     sharded over g >= 4 ranks, where a rank's small MSMs are latency-bound; beside the commitment otherwise"""
@@ -658,6 +679,23 @@ def main():
     # headline configuration
     hctxs, hpk = (sctxs, spk) if sharded_head else (ctxs, pk)
     hctx = hctxs[0]
+    # proofs in flight capped by device memory: one probe proof (uncached and index-cached) on the
+    # first context measures a context's footprint; every rank keeps the same count (min over ranks)
+    def probe():
+        for cached in (False, True):
+            spx.MLArgumentForR1CS.prove_witness(hpk, wits[0], pp, mode=args.mode, seed=7, cached=cached,
+                                                commitment_stub=stub)
+    nfit, mem_fit = fit_inflight(hctxs, probe)
+    if dist is not None:
+        import torch
+
+        tf = torch.tensor([nfit], dtype=torch.int64)
+        dist.all_reduce(tf, op=dist.ReduceOp.MIN)
+        nfit = int(tf[0])
+    if nfit < len(hctxs):
+        sys.stderr.write("bench.py: %d of %d contexts fit the device memory (%s)\n" % (nfit, len(hctxs), mem_fit))
+        del hctxs[nfit:]
+    mem_fit["contexts"] = len(hctxs)
     batch_fn(hctxs, hpk, max(1, args.warmup))()
     if not args.no_stats:
         spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
@@ -723,9 +761,14 @@ def main():
                 c.set_comm_shm("%s_g%d_%d" % (gname[0], rank // K, j), rank % K, K)
             gpk = spx.IndexPK(gctxs[0], index_from_c(spx, gctxs[0], mats), log_n)
             batch_fn(gctxs, gpk, 1)()
-            pg, elg = timed(batch_fn(gctxs, gpk, args.steps))
+            pg, elg = timed(batch_fn(gctxs, gpk, args.steps), "groups_%d" % K)
             check_batch(pg, ref)
-            grouped[K] = elg
+            # the same groups with the index-cached transcript: a group's K ranks absorb the matrices
+            # of all its proofs (proof i by its rank i mod K), i.e. N / K times the hashing of the
+            # proof-sharded headline on the same host; this separates that host cost from the GPU's
+            pgc, elgc = timed(batch_fn(gctxs, gpk, args.steps, cached=True), "groups_%d_index_cached" % K)
+            check_batch(pgc, ref)
+            grouped[K] = (elg, elgc)
             del gctxs, gpk
 
     # ---- N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank (rank 0 of G) of every
@@ -766,9 +809,9 @@ def main():
         import torch
 
         for K in sorted(grouped):  # max over ranks, in the same order on every rank
-            tg = torch.tensor([grouped[K] / args.steps * 1e3], dtype=torch.float64)
+            tg = torch.tensor([grouped[K][0] / args.steps * 1e3, grouped[K][1] / args.steps * 1e3], dtype=torch.float64)
             dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-            ms_g[K] = float(tg[0])
+            ms_g[K] = (float(tg[0]), float(tg[1]))
         t = torch.tensor([ms, ms_c, ms_1, ms_1c, (other[0] / args.steps * 1e3) if other else 0.0,
                           (other[1] / args.steps * 1e3) if other and other[1] else 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -870,6 +913,7 @@ def main():
             # the first witness's proof byte-equal to the test oracle's, proved in this run (cpu_baseline_all_cores)
             "parity_2_%d" % log_n: parity,
             "ranks_seen": ranks_seen,
+            "device_memory": mem_fit,
         }
         if hub_stats is not None:
             out["comm_%s_hub_stats_rank0" % args.comm] = hub_stats
@@ -887,9 +931,10 @@ def main():
                        "hashing_wait_ms_per_proof": round((hs1[3] - hs0[3]) / pool_n * 1e3, 2) if pool_n else None,
                        # the whole process's CPU use (proof workers, HIP runtime, hashing pool) in cores
                        "process_cores_busy": cpu_busy}
-        for K, mg in ms_g.items():
+        for K, (mg, mgc) in ms_g.items():
             out.setdefault("value_proof_groups", {})[str(K)] = {
                 "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),
+                "value_index_cached_transcript": round(P * (world // K) * n / (mgc / 1e3), 1),
                 "layout": "%d groups of %d ranks, every proof sharded over its group (%d proofs per group per step)" % (
                     world // K, K, P)}
         if ms_o is not None:

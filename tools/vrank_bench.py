@@ -61,6 +61,12 @@ def main():
     [t.join() for t in ths]
     wits = [spx.Witness(ctxs[0][0], z[: 32 << a.log_v], z[32 << a.log_v :]) for z in zs]
     del zs
+    mem = None
+    if a.solo:  # proofs in flight capped by device memory, as bench.py does (one probe proof on context 0)
+        nfit, mem = bench.fit_inflight(ctxs[0], lambda: spx.MLArgumentForR1CS.prove_witness(
+            pks[0], wits[0], pp, cached=a.cached))
+        del ctxs[0][nfit:]
+        B = len(ctxs[0])
 
     def run(steps):
         out = [None] * G
@@ -73,24 +79,25 @@ def main():
                 errs.append(repr(e))
 
         t = [threading.Thread(target=rank, args=(r,)) for r in range(G)]
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.process_time()
         [x.start() for x in t]
         [x.join() for x in t]
         el = time.perf_counter() - t0
         assert not errs, errs
         assert all(o == out[0] for o in out), "ranks disagree"
-        return out[0], el
+        return out[0], el, time.process_time() - c0
 
     if a.warmup:
         run(a.warmup)
-    proofs, el = run(a.steps)
+    proofs, el, cpu = run(a.steps)
     print(json.dumps({"G": world, "solo_rank0": a.solo, "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
                       "value": round(a.steps * P * n / el, 1), "ms_per_proof": round(el / (a.steps * P) * 1e3, 3),
                       # strong scaling: every rank works on every proof, so the node finishes the batch when
                       # rank 0 does (ranks are symmetric; exchanges taken as free)
                       "node_estimate": round(a.steps * P * n / el, 1) if a.solo else None,
                       "distinct": len(set(proofs)),
-                      "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs)}), flush=True)
+                      "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs), "device_memory": mem,
+                      "process_cores_busy": round(cpu / el, 2)}), flush=True)
 
 
 if __name__ == "__main__":

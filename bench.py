@@ -49,6 +49,14 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_kernels.json")
 # the same passes over the C2 workload (2^18, commitment stubbed): its launches' own counters
 PMC_FILE_C2 = os.path.join(ROOT, "profiles", "pmc_kernels_c2.json")
 ISSUE_FILE = os.path.join(ROOT, "profiles", "r02_ubench_issue.txt")
+# effective shader clock of the long kernels (rocprofv3 --pmc GRBM_GUI_ACTIVE + the same pass's kernel
+# trace, one proof in flight: tools/pmc_clock.sh; MI355X_MICROARCH.md "DVFS give-back")
+CLOCK_FILE = os.path.join(ROOT, "profiles", "r05", "r05a_clock.json")
+# the oracle's reference-faithful prover on ONE core at the metric's 2^20 on the GPU box (~220 s, too
+# long for every bench run: tools/cpu_baseline_1core.py, run once, proof byte-equal to the GPU's)
+CPU1_2_20_FILE = os.path.join(ROOT, "profiles", "r05", "r05a_cpu_baseline_1core_2_20.json")
+# BASELINE C5 (2^24, 8 ranks) byte parity and the oracle's 16-core time there (tools/c5_parity.py)
+C5_FILE = os.path.join(ROOT, "profiles", "r05", "r05d_c5_parity_2_24.json")
 MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
@@ -262,6 +270,21 @@ def roofline_valu(stats, dom):
             roof["mix_ceiling_cycles_per_instr"] = round(mix, 2)
             roof["achieved_cycles_per_instr"] = round(avg_s * 1024 * 2.4e9 / insts, 2)
             roof["frac_vs_mix_ceiling"] = round(insts * mix / (1024 * 2.4e9) / avg_s, 4)
+    clk = held_clock(KSYM.get(dom, dom))
+    if clk and insts:
+        # the clock the chip holds under this kernel (GRBM_GUI_ACTIVE / 8 / duration in the PMC pass),
+        # carried to the live duration at the same cycle count: the issue peak and the cycles per
+        # instruction at that clock instead of the 2.4 GHz maximum
+        f = clk["effective_clock_GHz"] * 1e9 * clk["mean_us"] / (avg_s * 1e6)
+        roof["held_clock"] = {
+            "GHz": round(f / 1e9, 3), "pmc_GHz": clk["effective_clock_GHz"], "pmc_mean_us": clk["mean_us"],
+            "peak_at_held_clock": round(1024 * f / 2.0 / 1e9, 1),
+            "frac_at_held_clock": round(insts / avg_s / (1024 * f / 2.0), 4),
+            "achieved_cycles_per_instr": round(avg_s * 1024 * f / insts, 3),
+            "source": os.path.relpath(CLOCK_FILE, ROOT) + " (tools/pmc_clock.sh)"}
+        if roof.get("mix_ceiling_cycles_per_instr"):
+            roof["held_clock"]["frac_vs_mix_ceiling"] = round(
+                roof["mix_ceiling_cycles_per_instr"] / roof["held_clock"]["achieved_cycles_per_instr"], 4)
     roof["hbm"] = {
         "algorithmic_bytes_per_launch": per_launch,
         "achieved_GBs": round(per_launch / avg_s / 1e9, 1),
@@ -312,6 +335,27 @@ def whole_proof_valu(ms_per_proof):
             "achieved": round(ach / 1e9, 1), "peak": round(VALU_PEAK_WAVE_INSTR / 1e9, 1), "unit": "G VALU wave-instructions/s",
             "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
             "source": "profiles/pmc_kernels.json (per-proof kernels of the PMC pass, %d proofs)" % proofs}
+
+
+def held_clock(sym):
+    """{effective_clock_GHz, mean_us} of kernel `sym` from the committed GRBM_GUI_ACTIVE pass"""
+    try:
+        ks = json.load(open(CLOCK_FILE))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for k, v in ks.items():  # "void spx::k_accum_aff<spx::Fe<spx::FqCfg> >" -> "k_accum_aff<Fq >"
+        if k.replace("void ", "").replace("spx::", "").replace("Fe<FqCfg>", "Fq") == sym:
+            return v
+    return None
+
+
+def committed_record(path):
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    d["source"] = os.path.relpath(path, ROOT)
+    return d
 
 
 def madd_register_resident():
@@ -922,6 +966,18 @@ def main():
         # (the pool's own clock over the timed region: multi-buffer lanes hash several proofs per job)
         hash_s = phases.get("transcript_matrices", 0.0) / 1e6
         pool_s, pool_n = hs1[0] - hs0[0], hs1[1] - hs0[1]
+        if world == 1 and log_n == 20 and not stub and args.kind == 3:
+            # the headline's baseline at the metric's own size: one core, 2^20 (committed record)
+            c1 = committed_record(CPU1_2_20_FILE)
+            if c1:
+                c1["gpu_value_over_it"] = round(out["value"] / c1["value"], 1)
+                out["cpu_baseline_1core_2_20"] = c1
+        c5 = committed_record(C5_FILE)
+        if c5 and not stub:
+            out["c5_parity_2_24"] = {"equal": c5.get("equal"), "ranks": c5.get("ranks"), "proof_bytes": c5.get("proof_bytes"),
+                                     "oracle_cores": c5.get("oracle_threads"), "oracle_s": c5.get("oracle_s"),
+                                     "oracle_constraints_per_s": round((1 << 24) / c5["oracle_s"], 1) if c5.get("oracle_s") else None,
+                                     "source": c5["source"]}
         out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
                        "hashing_lanes": hs1[2],
                        "hashing_core_s_per_proof": round(pool_s / pool_n, 4) if pool_n else None,

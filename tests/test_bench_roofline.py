@@ -72,3 +72,26 @@ def test_hbm_largest_launch_rates(bench):
     assert r["us"] == pytest.approx(50.0)
     assert r["GBs"] == pytest.approx(3520.0)
     assert r["frac"] == pytest.approx(0.44)
+
+
+def test_held_clock_restates_the_roofline(bench):
+    """the GRBM_GUI_ACTIVE pass's clock carried to the live launch duration: at the measured duration of
+    the PMC pass itself the held clock is the pass's clock, and the cycles per instruction follow"""
+    clk = bench.held_clock("k_accum_aff<Fq2>")
+    assert clk and 1.5 < clk["effective_clock_GHz"] < 2.5
+    pm = _pmc()["k_accum_aff<Fq2>"]
+    alg = pm["alg_bytes_per_launch"]
+    ms = clk["mean_us"] / 1e3
+    r = bench.roofline_valu({"msm_acc_g2": {"launches": 1.0, "ms": ms, "bytes": alg, "ops": 0.0}}, "msm_acc_g2")
+    h = r["held_clock"]
+    assert h["GHz"] == pytest.approx(clk["effective_clock_GHz"], rel=1e-3)
+    want = ms * 1e-3 * 1024 * clk["effective_clock_GHz"] * 1e9 / r["valu_insts_per_launch"]
+    assert h["achieved_cycles_per_instr"] == pytest.approx(want, rel=1e-3)
+    assert h["frac_at_held_clock"] > r["frac"]  # the held clock's peak is below the 2.4 GHz one
+
+
+def test_committed_cpu_baselines(bench):
+    c1 = bench.committed_record(bench.CPU1_2_20_FILE)
+    assert c1["cores"] == 1 and c1["log_n"] == 20 and c1["parity_vs_gpu"] is True
+    c5 = bench.committed_record(bench.C5_FILE)
+    assert c5["equal"] is True and c5["log_n"] == 24 and c5["ranks"] == 8

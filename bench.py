@@ -425,6 +425,16 @@ def hw_queues_for(g):
     return 4 if g <= 2 else 32
 
 
+def sync_poll_for(g):
+    """SPX_SYNC_POLL_US for proofs sharded over g ranks: host waits poll an event every 50 us instead of
+    spinning in the HSA runtime (~0.2 ms of a core per wait). A rank of a g-rank proof replays every
+    proof's host work at g times the single-GPU proof rate: at g = 8 the spinning took ~9 of its 16
+    cores; polling halves the proving threads' CPU at equal throughput (profiles/r05/r05g_poll.jsonl,
+    r05h_poll_inflight.jsonl). At g <= 2 the spinning has cores to spare and polling adds ~40 us per
+    wait to a proof's latency: kept off."""
+    return 50 if g >= 4 else 0
+
+
 # device memory kept free beyond the contexts' own footprint (HIP runtime, fragmentation, the
 # index-cached runs' second-stream MSM workspace, per-launch temporaries)
 FIT_RESERVE = 8 << 30
@@ -621,6 +631,7 @@ def main():
     # otherwise, so an A/B can vary it)
     if world >= 4:
         os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues_for(world))
+        os.environ.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(world)))
     else:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
     spx = load_product()
@@ -744,9 +755,9 @@ def main():
     if not args.no_stats:
         spx._check(L.spx_kernel_stats_enable(hctx.h, 1))
     # ---- timed region (headline): K steps x P full proofs, pipelined over B workers
-    hs0 = spx.hash_stats()
+    hs0, hp0 = spx.hash_stats(), spx.host_phase_stats()
     proofs, elapsed = timed(batch_fn(hctxs, hpk, args.steps), "headline")
-    hs1 = spx.hash_stats()
+    hs1, hp1 = spx.hash_stats(), spx.host_phase_stats()
     stats = {}
     if not args.no_stats:
         stats = kernel_stats(spx, L, hctx, args.steps * (P // len(hctxs)))  # ctx 0 proves P / B proofs per step
@@ -831,6 +842,7 @@ def main():
                      "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "msm_reruns": {}}
         for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
             env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues_for(G)))
+            env.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(G)))
             cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo",
                    "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P), "--steps", str(args.steps),
                    "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
@@ -986,7 +998,11 @@ def main():
                        # summed over the proof workers: time a proof waited for its absorption
                        "hashing_wait_ms_per_proof": round((hs1[3] - hs0[3]) / pool_n * 1e3, 2) if pool_n else None,
                        # the whole process's CPU use (proof workers, HIP runtime, hashing pool) in cores
-                       "process_cores_busy": cpu_busy}
+                       "process_cores_busy": cpu_busy,
+                       # the proving threads' CPU per proof by prove() phase over the headline run (ms); a
+                       # rank of a sharded proof does all of it for every proof (it does not divide by N)
+                       "proving_thread_cpu_ms_per_proof": {
+                           k: round((hp1[k][0] - hp0[k][0]) / max(1, len(proofs)) * 1e3, 3) for k in hp1}}
         for K, (mg, mgc) in ms_g.items():
             out.setdefault("value_proof_groups", {})[str(K)] = {
                 "value": round(P * (world // K) * n / (mg / 1e3), 1), "ms_per_step": round(mg, 3),

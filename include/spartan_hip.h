@@ -198,6 +198,10 @@ int spx_prover_free(spx_prover *p);
  * lane width (proofs hashed per vector instruction: 16 AVX-512, 8 AVX2, 1 scalar), out[3] nanoseconds
  * the proof workers waited for a proof's absorption (summed over the workers) */
 int spx_hash_stats(uint64_t out[4]);
+/* host CPU of the proving threads by prove() phase, process-wide since load: out[3 i], out[3 i + 1],
+ * out[3 i + 2] = thread CPU ns, wall ns and count of phase i in the order transcript_matrices, commit,
+ * open_rv, sumcheck1, eval_on_x, sumcheck2, open_ry (the phases of spx_last_timings) */
+int spx_host_phase_stats(uint64_t out[21]);
 /* MLArgumentForR1CS::verify (src/lib.rs:147-212, verifier.rs:143-512): SPX_OK = accepted (the
  * reference's Ok(true)); a rejection returns the reference's error kind (SPX_INVALID_ARGUMENT,
  * SPX_SUMCHECK, SPX_WRONG_WITNESS, SPX_SERIALIZATION) with its message in spx_last_error.

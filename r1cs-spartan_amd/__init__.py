@@ -94,6 +94,7 @@ EXPORTED = [
     "spx_ctx_comm_allgather",
     "spx_msm_reruns",
     "spx_ctx_mem_info",
+    "spx_host_phase_stats",
     "spx_pp_load",
     "spx_pp_generate",
     "spx_pp_serialize",
@@ -461,6 +462,17 @@ def hash_stats():
     out = (ctypes.c_uint64 * 4)()
     _check(lib().spx_hash_stats(out))
     return out[0] / 1e9, out[1], out[2], out[3] / 1e9
+
+
+HOST_PHASES = ["transcript_matrices", "commit", "open_rv", "sumcheck1", "eval_on_x", "sumcheck2", "open_ry"]
+
+
+def host_phase_stats():
+    """{phase: (thread CPU s, wall s, count)} of prove() on this process's proving threads
+    (spx_host_phase_stats; cumulative since load)"""
+    a = (ctypes.c_uint64 * 21)()
+    _check(lib().spx_host_phase_stats(a))
+    return {p: (a[3 * i] / 1e9, a[3 * i + 1] / 1e9, a[3 * i + 2]) for i, p in enumerate(HOST_PHASES)}
 
 
 def shm_name():

@@ -529,6 +529,12 @@ int spx_hash_stats(uint64_t out[4]) {
         out[3] = g_hash_wait_ns.load();
     });
 }
+int spx_host_phase_stats(uint64_t out[21]) {
+    return guard([&] {
+        if (!out) spx::invalid("null argument");
+        spx::host_phase_stats(out);
+    });
+}
 int spx_vp_from_pp(spx_pp* pp, uint8_t* out, size_t cap, size_t* len) {
     return guard([&] {
         if (!pp) spx::invalid("null public parameter");

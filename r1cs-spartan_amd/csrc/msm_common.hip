@@ -450,7 +450,11 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     const int nact = (int)p.insts.size();
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
     o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(n, 1));
+#ifdef SPX_AB_RADIX_COMPACT
+    if (false) {
+#else
     if (p.compact) {  // counting sort: keys + counts, every offset array in one workgroup, scatter
+#endif
         if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
         uint32_t* hist = (uint32_t*)ws->hist.ensure(4 * (size_t)std::max<uint32_t>(nb, 1));
         if (ws->hist_zeroed != ws->hist.cap) {  // fresh allocation: zero once; the offsets kernel keeps it zero
@@ -486,8 +490,12 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     // (a counting sort, histogram atomics in the keys pass + scan + scatter, measured 10% slower end to
     // end: profiles/r03/r03t_ab.jsonl; 11-bit onesweep digits no faster: r03at_ab_sort_bits.jsonl)
     kp_begin(KP_SORT, s);
-    hipLaunchKernelGGL((k_msm_keys<false, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
-                       nb, scalars, ka, va, 0u, st, nullptr, nullptr);
+    if (p.compact)
+        hipLaunchKernelGGL((k_msm_keys<true, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
+                           nb, scalars, ka, va, (uint32_t)n, st, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((k_msm_keys<false, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
+                           nb, scalars, ka, va, 0u, st, nullptr, nullptr);
     {
         hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
         size_t tb = 0;

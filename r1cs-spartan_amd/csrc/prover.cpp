@@ -16,7 +16,10 @@
 #include <type_traits>
 
 #include <algorithm>
+#include <sys/prctl.h>
+
 #include <chrono>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 
@@ -45,6 +48,37 @@ Ctx::Ctx(int dev) : device(dev) {
     msm = msm_ws_create();
     comm.reset(new LocalComm());
 }
+// SPX_SYNC_POLL_US (see Ctx::wait_stream): 0 = hipStreamSynchronize
+static int sync_poll_us() {
+    static const int v = [] {
+        const char* e = getenv("SPX_SYNC_POLL_US");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    return v;
+}
+void Ctx::wait_stream(hipStream_t s, hipEvent_t& ev) {
+    const int us = sync_poll_us();
+    if (us <= 0) {
+        SPX_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    thread_local bool slack_set = false;
+    if (!slack_set) {  // sleeps of tens of microseconds, not the default 50 us timer slack on top
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+        slack_set = true;
+    }
+    if (!ev) SPX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    SPX_HIP(hipEventRecord(ev, s));
+    for (int i = 0;; ++i) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) SPX_HIP(e);
+        if (i < 4)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(us));
+    }
+}
 void Ctx::ensure_side() {
     if (side) return;
     SPX_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
@@ -53,6 +87,8 @@ void Ctx::ensure_side() {
 }
 Ctx::~Ctx() {
     (void)hipSetDevice(device);
+    if (wait_ev) (void)hipEventDestroy(wait_ev);
+    if (wait_ev_side) (void)hipEventDestroy(wait_ev_side);
     if (msm_side) msm_ws_destroy(msm_side);
     if (side_ev) (void)hipEventDestroy(side_ev);
     if (side) (void)hipStreamDestroy(side);
@@ -714,6 +750,26 @@ struct Timer {
     }
 };
 
+// Host CPU of the proving threads by phase, process-wide (spx_host_phase_stats): the calling thread's
+// CPU time (CLOCK_THREAD_CPUTIME_ID) between prove()'s phase marks, with the wall time and the count.
+// A rank of a G-rank proof replays the whole transcript and host arithmetic of every proof while its
+// device work is 1/G, so this host work is what does not divide when proofs are sharded.
+static uint64_t thread_cpu_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+static const char* const kPhaseNames[kHostPhases] = {"transcript_matrices", "commit", "open_rv", "sumcheck1",
+                                                     "eval_on_x", "sumcheck2", "open_ry"};
+static std::atomic<uint64_t> g_phase_cpu[kHostPhases], g_phase_wall[kHostPhases], g_phase_cnt[kHostPhases];
+void host_phase_stats(uint64_t* out) {  // [phase][cpu ns, wall ns, count]
+    for (int i = 0; i < kHostPhases; ++i) {
+        out[3 * i] = g_phase_cpu[i].load();
+        out[3 * i + 1] = g_phase_wall[i].load();
+        out[3 * i + 2] = g_phase_cnt[i].load();
+    }
+}
+
 // device MSM output (XYZZ, R = 2^384 Montgomery limbs) -> host Jacobian without an inversion:
 // Z = ZZ ZZZ, X = x Z^2 = X ZZ ZZZ^2, Y = y Z^3 = Y ZZ^3 ZZZ^2 (ZZ = 0: infinity)
 template <class F>
@@ -1043,9 +1099,20 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     } drain{C};
     Timer tall;
     C.timings.clear();
+    int phase = 0;
+    uint64_t cpu0 = thread_cpu_ns();
     auto mark = [&](const char* name, Timer& t) {
-        C.timings.emplace_back(name, t.us());
+        const double us = t.us();
+        C.timings.emplace_back(name, us);
         t = Timer();
+        const uint64_t c1 = thread_cpu_ns();
+        if (phase < kHostPhases) {
+            g_phase_cpu[phase] += c1 - cpu0;
+            g_phase_wall[phase] += (uint64_t)(us * 1e3);
+            g_phase_cnt[phase] += 1;
+        }
+        ++phase;
+        cpu0 = c1;
     };
     Timer tp;
     const int L = I.log_n;

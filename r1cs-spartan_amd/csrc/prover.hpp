@@ -197,14 +197,20 @@ struct Ctx {
     ~Ctx();
     // region [off, off + bytes) of the pinned carve-out (throws if it does not fit its region)
     uint8_t* pin_at(size_t off, size_t bytes, size_t region);
+    // Waits for a stream's queued work. hipStreamSynchronize under the blocking-sync flag still spins
+    // in the HSA runtime before it sleeps (~0.2 ms of a core per wait): with 64 proofs in flight per
+    // rank and ~45 waits per proof that spinning was most of a proof's host CPU. With SPX_SYNC_POLL_US
+    // = t > 0 the wait records an event and polls it, sleeping t us between polls (wait_stream).
+    hipEvent_t wait_ev = nullptr, wait_ev_side = nullptr;
+    void wait_stream(hipStream_t s, hipEvent_t& ev);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
-        SPX_HIP(hipStreamSynchronize(stream));
+        wait_stream(stream, wait_ev);
         msm_ws_staging_reset(msm);
         if (kprof.on) kprof.harvest();
     }
     void side_sync() {
         if (!side) return;
-        SPX_HIP(hipStreamSynchronize(side));
+        wait_stream(side, wait_ev_side);
         msm_ws_staging_reset(msm_side);
     }
 };
@@ -325,6 +331,10 @@ struct ProveOpts {
 Blake2s absorb_matrices(const Index& I);
 // the same absorption for k proofs at once (multi-buffer BLAKE2s: k equal states in vector lanes)
 void absorb_matrices_lanes(const Index& I, Blake2s* out, int k);
+
+// host CPU of prove()'s phases, process-wide: out[3 i .. 3 i + 2] = CPU ns, wall ns, count of phase i
+static constexpr int kHostPhases = 7;
+void host_phase_stats(uint64_t* out);
 
 // entry points used by the C ABI
 std::unique_ptr<PP> pp_load(Ctx& C, const uint8_t* b, size_t len);

@@ -60,6 +60,7 @@ def test_settings_by_sharding_degree(bench):
     assert [bench.inflight_for(g) for g in (1, 2, 4, 8, 16)] == [32, 32, 32, 64, 64]
     assert [bench.hw_queues_for(g) for g in (1, 2, 4, 8)] == [4, 4, 32, 32]
     assert [bench.lvl0_for(g) for g in (1, 2, 4, 8)] == [0, 0, 1, 1]
+    assert [bench.sync_poll_for(g) for g in (1, 2, 4, 8)] == [0, 0, 50, 50]
     for g in (1, 2, 4, 8):
         assert 64 % bench.inflight_for(g) == 0
         assert bench.hw_queues_for(g) <= 32  # gpurun / the pool refuse more

@@ -34,6 +34,7 @@ def main():
     a = ap.parse_args()
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    os.environ.setdefault("SPX_SYNC_POLL_US", str(bench.sync_poll_for(a.G)))
     spx = bench.load_product()
     G, B, P = a.G, a.inflight or bench.inflight_for(a.G), a.proofs
     world = G
@@ -89,7 +90,12 @@ def main():
 
     if a.warmup:
         run(a.warmup)
+    hp0 = spx.host_phase_stats()
     proofs, el, cpu = run(a.steps)
+    hp1 = spx.host_phase_stats()
+    npf = max(1, len(proofs))
+    host_phases = {k: {"cpu_ms": round((hp1[k][0] - hp0[k][0]) / npf * 1e3, 3),
+                       "wall_ms": round((hp1[k][1] - hp0[k][1]) / npf * 1e3, 3)} for k in hp1}
     print(json.dumps({"G": world, "solo_rank0": a.solo, "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
                       "value": round(a.steps * P * n / el, 1), "ms_per_proof": round(el / (a.steps * P) * 1e3, 3),
                       # strong scaling: every rank works on every proof, so the node finishes the batch when
@@ -97,7 +103,10 @@ def main():
                       "node_estimate": round(a.steps * P * n / el, 1) if a.solo else None,
                       "distinct": len(set(proofs)),
                       "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs), "device_memory": mem,
-                      "process_cores_busy": round(cpu / el, 2)}), flush=True)
+                      "process_cores_busy": round(cpu / el, 2),
+                      "process_cpu_ms_per_proof": round(cpu / npf * 1e3, 3),
+                      # per proof, on the proving threads (prove()'s phases), excluding the hashing pool
+                      "host_phases_per_proof": host_phases}), flush=True)
 
 
 if __name__ == "__main__":

@@ -177,32 +177,32 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
 // A proof-sharded rank keeps 1/G of the digits (G = 8 at 2^20: ~2 M pairs per batch into 2^12..2^16
 // local buckets). Their order is: keys pass (hist[key]++ gives each pair its rank in its bucket) ->
 // ONE workgroup derives every offset array from the counts -> one scatter pass. Three launches, no
-// device-wide look-back scans, no fill kernels; the radix sort stays for dense batches.
+// device-wide look-back scans, no fill kernels; the radix sort stays for dense batches and for
+// 2-rank sharding (MsmPlan::counting).
 static constexpr int kScanThreads = 1024;
 static constexpr int kMaxLev = 8;
 struct LevPtrs {
     uint32_t* p[kMaxLev + 1];  // [0]: the affine level's partial offsets; [l]: XYZZ level l
 };
-// exclusive scan of value(b), b = 0..n-1, over one workgroup (each thread a contiguous chunk); writes
-// out[b] (0 everywhere when `zero`); returns the total (every thread). Ends with a barrier, so `out`
-// is visible to the whole workgroup afterwards.
-template <class V>
-DEV uint32_t wg_scan(uint32_t n, V value, uint32_t* __restrict__ out, bool zero) {
-    using Scan = hipcub::BlockScan<uint32_t, kScanThreads>;
-    __shared__ typename Scan::TempStorage tmp;
-    const uint32_t E = (n + kScanThreads - 1) / kScanThreads;
-    const uint32_t b0 = min(n, threadIdx.x * E), b1 = min(n, b0 + E);
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += value(b);
-    uint32_t pre, agg;
-    Scan(tmp).ExclusiveSum(sum, pre, agg);
-    for (uint32_t b = b0; b < b1; ++b) {
-        out[b] = zero ? 0u : pre;
-        pre += value(b);
+// The offsets kernel runs in ONE workgroup of kScanThreads threads and goes through the counts in
+// tiles of kScanThreads x kScanPer buckets (thread t: kScanPer consecutive buckets). Every array it
+// writes is an exclusive scan of a per-bucket count that follows from the bucket's own reference
+// count c and its offset o: the affine level's partials p = c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0
+// (the seg1-reference thread ranges [o, o + c) meets), and each XYZZ level's segments
+// ceil(previous count / kSeg). So a tile needs two block scans (offsets, then all partial arrays
+// at once as one vector) and the counts are read once.
+static constexpr int kScanPer = 8;
+struct ScanVec {
+    uint32_t v[kMaxLev + 1];
+};
+struct ScanVecSum {
+    DEV ScanVec operator()(const ScanVec& a, const ScanVec& b) const {
+        ScanVec r;
+#pragma unroll
+        for (int k = 0; k <= kMaxLev; ++k) r.v[k] = a.v[k] + b.v[k];
+        return r;
     }
-    __syncthreads();
-    return agg;
-}
+};
 // hist (nb counts) -> offs (nb + 1), lev.p[0] (partials of seg1-reference thread ranges) and
 // lev.p[1..nlev] (segments of kSeg partials), exactly the arrays scan_partials / scan_segs give the
 // dense path; hist is cleared for the next batch. If the counted pairs exceed the capacity (the
@@ -211,30 +211,80 @@ DEV uint32_t wg_scan(uint32_t n, V value, uint32_t* __restrict__ out, bool zero)
 __global__ __launch_bounds__(kScanThreads) void k_msm_offsets(uint32_t* __restrict__ hist, uint32_t nb, uint32_t cap,
                                                               uint32_t* __restrict__ st, uint32_t* __restrict__ offs,
                                                               uint32_t seg1, int nlev, LevPtrs lev) {
+    using Red = hipcub::BlockReduce<uint32_t, kScanThreads>;
+    using Scan1 = hipcub::BlockScan<uint32_t, kScanThreads>;
+    using ScanV = hipcub::BlockScan<ScanVec, kScanThreads>;
+    __shared__ union {
+        typename Red::TempStorage r;
+        typename Scan1::TempStorage a;
+        typename ScanV::TempStorage v;
+    } tmp;
     __shared__ uint32_t s_total;
     {  // pass 1: the total, to decide overflow before anything is written
-        using Red = hipcub::BlockReduce<uint32_t, kScanThreads>;
-        __shared__ typename Red::TempStorage rt;
         uint32_t sum = 0;
         for (uint32_t b = threadIdx.x; b < nb; b += kScanThreads) sum += hist[b];
-        const uint32_t t = Red(rt).Sum(sum);
+        const uint32_t t = Red(tmp.r).Sum(sum);
         if (threadIdx.x == 0) s_total = t;
         __syncthreads();
     }
     const bool over = s_total > cap;
     if (over && threadIdx.x == 0) atomicOr(&st[0], kMsmOverflow);
-    wg_scan(nb + 1, [&](uint32_t b) { return b < nb ? hist[b] : 0u; }, offs, over);
-    for (uint32_t b = threadIdx.x; b < nb; b += kScanThreads) hist[b] = 0u;
-    const uint32_t* prev = offs;
-    wg_scan(nb + 1, [&](uint32_t b) -> uint32_t {
-        if (b >= nb) return 0u;
-        const uint32_t o = prev[b], c = prev[b + 1] - o;
-        return c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0u;
-    }, lev.p[0], over);
-    for (int l = 1; l <= nlev; ++l) {
-        const uint32_t* pv = lev.p[l - 1];
-        wg_scan(nb + 1, [&](uint32_t b) -> uint32_t { return b < nb ? (pv[b + 1] - pv[b] + kSeg - 1) / kSeg : 0u; },
-                lev.p[l], over);
+    const uint32_t n = nb + 1;  // offs[nb] / lev[l][nb]: the totals
+    uint32_t carry0 = 0;
+    ScanVec carry;
+#pragma unroll
+    for (int l = 0; l <= kMaxLev; ++l) carry.v[l] = 0;
+    for (uint32_t base = 0; base < n; base += kScanThreads * kScanPer) {
+        const uint32_t b0 = base + threadIdx.x * kScanPer;
+        uint32_t c[kScanPer], s = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            c[k] = b0 + k < nb ? hist[b0 + k] : 0u;
+            s += c[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+            if (b0 + k < nb) hist[b0 + k] = 0u;
+        uint32_t e0, agg0;
+        Scan1(tmp.a).ExclusiveSum(s, e0, agg0);
+        __syncthreads();
+        // this thread's partial-array counts, summed per array
+        ScanVec sv;
+#pragma unroll
+        for (int l = 0; l <= kMaxLev; ++l) sv.v[l] = 0;
+        uint32_t o = carry0 + e0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            uint32_t v = c[k] ? (o + c[k] - 1) / seg1 - o / seg1 + 1 : 0u;
+            sv.v[0] += v;
+            for (int l = 1; l <= nlev; ++l) {
+                v = (v + kSeg - 1) / kSeg;
+                sv.v[l] += v;
+            }
+            o += c[k];
+        }
+        ScanVec ev, aggv;
+        ScanV(tmp.v).ExclusiveScan(sv, ev, carry, ScanVecSum(), aggv);  // carry as the initial value
+        __syncthreads();
+        o = carry0 + e0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const uint32_t b = b0 + k;
+            if (b < n) {
+                offs[b] = over ? 0u : o;
+                uint32_t v = c[k] ? (o + c[k] - 1) / seg1 - o / seg1 + 1 : 0u;
+                lev.p[0][b] = over ? 0u : ev.v[0];
+                ev.v[0] += v;
+                for (int l = 1; l <= nlev; ++l) {
+                    v = (v + kSeg - 1) / kSeg;
+                    lev.p[l][b] = over ? 0u : ev.v[l];
+                    ev.v[l] += v;
+                }
+            }
+            o += c[k];
+        }
+        carry0 += agg0;
+        carry = ScanVecSum()(carry, aggv);
     }
 }
 // compacted pair i -> refs[offs[key] + its rank in the bucket] (skipped when the batch overflowed)
@@ -345,6 +395,11 @@ MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_sc
     while ((1 << g) < G) ++g;
     if ((1 << g) != G || sh.rank < 0 || sh.rank >= G) throw std::runtime_error("MSM shard: bad rank / world");
     o.compact = G > 1 && !sh.dense;
+    // the counting sort for 4 and more ranks (2^20: 2-3.5% more proofs per second than the radix sort
+    // at G = 8, equal at G = 4); at G = 2 a rank keeps half the digits (~8 M pairs per opening batch
+    // into ~10^5 buckets) and the returning bucket atomics and the one-workgroup offsets cost more than
+    // the radix sort does (105 vs 114 M constraints/s): profiles/r05/r05l_*.jsonl, r05m_*.jsonl
+    o.counting = o.compact && G >= 4;
     uint64_t tot_refs = 0;
     double split_refs = 0, whole_refs = 0;
     int nsplit = 0;
@@ -450,11 +505,7 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32
     const int nact = (int)p.insts.size();
     o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
     o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(n, 1));
-#ifdef SPX_AB_RADIX_COMPACT
-    if (false) {
-#else
-    if (p.compact) {  // counting sort: keys + counts, every offset array in one workgroup, scatter
-#endif
+    if (p.counting) {  // counting sort: keys + counts, every offset array in one workgroup, scatter
         if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
         uint32_t* hist = (uint32_t*)ws->hist.ensure(4 * (size_t)std::max<uint32_t>(nb, 1));
         if (ws->hist_zeroed != ws->hist.cap) {  // fresh allocation: zero once; the offsets kernel keeps it zero

@@ -128,6 +128,7 @@ struct MsmPlan {
     uint64_t tot_sc = 0;          // scalars digitised
     uint64_t tot_refs = 0;        // key slots: upper bound of the references with a digit in range
     bool compact = false;         // proof-sharded keys (only in-range digits, capacity tot_refs)
+    bool counting = false;        // compacted keys placed by the counting sort (else the radix sort)
     double mu_max = 0;            // largest expected references per bucket over the active instances
     bool any_split = false;
     // weighting tree: per instance, node offset and node count after the chunked leaf; levels above it

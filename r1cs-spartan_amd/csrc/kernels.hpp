@@ -49,6 +49,17 @@ struct ColStreamView {
     const Fr* val;           // entry slots: Montgomery values
     uint32_t nslices;
 };
+// sum_over_y for matrices whose every row has at most one entry (the R1CS multiplication-gate form;
+// the benchmark generators): the entries of the rank's rows of A, B and C, with an explicit zero entry
+// for an empty (row, matrix), sorted by column. Workgroups of XCD d take the d-th eighth of the list
+// (k_spmv_sliced), so each XCD gathers a contiguous eighth of z through its own L2, nearly in order,
+// instead of every XCD fetching whole 128-byte lines of z for 32-byte reads (k_sparse3<0>: 2.0x its
+// algorithmic bytes).
+struct SpmvSlicedView {
+    const Fr* val;        // [entries] Montgomery values
+    const uint32_t* col;  // [entries] global column, ascending
+    const uint32_t* dst;  // [entries] local row | matrix << 30
+};
 // per-block partial sums of one sumcheck round (3 Fr per block, up to 8192 blocks)
 static constexpr uint64_t kRoundPartials = 3 * 8192;
 
@@ -140,6 +151,7 @@ enum { KP_SC1 = 0, KP_SC2, KP_SPMV, KP_MTV, KP_OPEN, KP_EQ, KP_SORT, KP_ACC_G1, 
 // ---- mle_kernels.hip
 void launch_to_mont(Fr* d, size_t n, int* err, hipStream_t s);
 void launch_from_mont(Fr* out, const Fr* in, size_t n, hipStream_t s);
+void launch_spmv_sliced(const SpmvSlicedView& v, const Fr* z, Fr* o0, Fr* o1, Fr* o2, uint64_t entries, hipStream_t s);
 void launch_sparse3(int mode, const SparseView3& mv, const Fr* vec, Fr* o0, Fr* o1, Fr* o2, const Fr* scale,
                     uint64_t count, const LongChunk* chunks, int nchunks, const LongRow* lrows, int nlrows,
                     Fr* partial, hipStream_t s);

@@ -437,6 +437,49 @@ static void upload_sparse(Ctx& C, DevSparse& D, const std::vector<uint64_t>* ptr
     }
 }
 
+// Rows [lo, lo + cnt) of A, B, C as the column-sorted entry list (kernels.hpp: SpmvSlicedView) when
+// every one of them has at most one entry: the entries by column, within a column in (matrix, row)
+// order; an empty (row, matrix) is a zero entry whose column is the row (a product of 0 without a
+// branch). Returns false, uploading nothing, otherwise (the CSR path then serves the SpMV).
+static bool upload_sliced(Ctx& C, DevSliced& S, const HostCsr* mats, uint64_t n, uint64_t lo, uint64_t cnt,
+                          int* err_dev) {
+    if (n < (1ull << 12)) return false;
+    for (int m = 0; m < 3; ++m)
+        for (uint64_t x = lo; x < lo + cnt; ++x)
+            if (mats[m].rp[x + 1] - mats[m].rp[x] > 1) return false;
+    auto col_of = [&](int m, uint64_t x) -> uint32_t {
+        const uint64_t k = mats[m].rp[x];
+        return mats[m].rp[x + 1] > k ? mats[m].col[k] : (uint32_t)x;
+    };
+    std::vector<uint64_t> start(n + 1, 0);  // counting sort by column
+    for (int m = 0; m < 3; ++m)
+        for (uint64_t x = lo; x < lo + cnt; ++x) ++start[col_of(m, x) + 1];
+    for (uint64_t c = 0; c < n; ++c) start[c + 1] += start[c];
+    const uint64_t E = start[n];
+    std::vector<uint32_t> col(E), dst(E);
+    std::vector<uint8_t> val(32 * E, 0);
+    for (int m = 0; m < 3; ++m)
+        for (uint64_t x = lo; x < lo + cnt; ++x) {
+            const uint32_t c = col_of(m, x);
+            const uint64_t e = start[c]++;
+            col[e] = c;
+            dst[e] = (uint32_t)(x - lo) | ((uint32_t)m << 30);
+            const uint64_t k = mats[m].rp[x];
+            if (mats[m].rp[x + 1] > k) memcpy(val.data() + 32 * e, mats[m].val.data() + 32 * k, 32);
+        }
+    S.val.alloc(32 * E);
+    S.col.alloc(4 * E);
+    S.dst.alloc(4 * E);
+    SPX_HIP(hipMemcpyAsync(S.val.p, val.data(), 32 * E, hipMemcpyHostToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(S.col.p, col.data(), 4 * E, hipMemcpyHostToDevice, C.stream));
+    SPX_HIP(hipMemcpyAsync(S.dst.p, dst.data(), 4 * E, hipMemcpyHostToDevice, C.stream));
+    launch_to_mont(S.val.as<Fr>(), E, err_dev, C.stream);
+    C.sync();  // host vectors go out of scope
+    S.entries = E;
+    S.on = true;
+    return true;
+}
+
 // CSC copy of M for eval_on_x (rows ascending within a column). The reference inserts every
 // (xy_combine(x, y), value) pair into a SparseMLExtensionMap (r1cs_reader.rs:98-108), so when a
 // row repeats a column only the LAST entry of that row survives; sum_over_y (r1cs_reader.rs:75-85)
@@ -660,7 +703,7 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
     std::vector<uint32_t> cols[3];
     std::vector<uint8_t> vals[3];
     for (int m = 0; m < 3; ++m) rps[m] = mats[m].rp;
-    {
+    if (!upload_sliced(C, I->rows_sliced, mats, n, lo, nl, err.as<int>())) {
         const std::vector<uint32_t>* ci[3] = {&mats[0].col, &mats[1].col, &mats[2].col};
         const std::vector<uint8_t>* vi[3] = {&mats[0].val, &mats[1].val, &mats[2].val};
         std::vector<uint32_t> c3[3];
@@ -1161,10 +1204,12 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
 
     // ---- SpMV Az, Bz, Cz (challenge-independent: queued first, overlaps the commit's host work)
     {
-        SparseView3 rv = I.rows.view();
         kp_begin(KP_SPMV, C.stream);
-        launch_sparse3(0, rv, z, Az, Bz, Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(), I.rows.nchunks,
-                       I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
+        if (I.rows_sliced.on)
+            launch_spmv_sliced(I.rows_sliced.view(), z, Az, Bz, Cz, I.rows_sliced.entries, C.stream);
+        else
+            launch_sparse3(0, I.rows.view(), z, Az, Bz, Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(), I.rows.nchunks,
+                           I.rows.lrows.as<LongRow>(), I.rows.nlrows, partial, C.stream);
         kp_end(I.rows_bytes, C.stream);
     }
     // The shared level-0 opening proof is launched right behind the commitment, before any challenge,
@@ -1822,13 +1867,17 @@ std::vector<uint8_t> k_sum_over_y(Ctx& C, const HostCsr& m, const uint8_t* z) {
     std::vector<uint8_t> vals[3] = {mats[0].val, mats[1].val, mats[2].val};
     DevMem err(sizeof(int)), zd(32 * n), out(32 * n * 3), part(32 * 4096);
     SPX_HIP(hipMemsetAsync(err.p, 0, 4, C.stream));
-    upload_sparse(C, D, rps, cols, vals, 0, n, err.as<int>());
+    DevSliced S;  // the same two paths as prove(): sliced entries for single-entry rows, else CSR
+    if (!upload_sliced(C, S, mats, n, 0, n, err.as<int>())) upload_sparse(C, D, rps, cols, vals, 0, n, err.as<int>());
     SPX_HIP(hipMemcpyAsync(zd.p, z, 32 * n, hipMemcpyHostToDevice, C.stream));
     launch_to_mont(zd.as<Fr>(), n, err.as<int>(), C.stream);
     Fr* o = out.as<Fr>();
     if (D.nchunks > (int)4096) part.alloc(32 * D.nchunks);
-    launch_sparse3(0, D.view(), zd.as<Fr>(), o, o + n, o + 2 * n, nullptr, n, D.chunks.as<LongChunk>(), D.nchunks,
-                   D.lrows.as<LongRow>(), D.nlrows, part.as<Fr>(), C.stream);
+    if (S.on)
+        launch_spmv_sliced(S.view(), zd.as<Fr>(), o, o + n, o + 2 * n, S.entries, C.stream);
+    else
+        launch_sparse3(0, D.view(), zd.as<Fr>(), o, o + n, o + 2 * n, nullptr, n, D.chunks.as<LongChunk>(), D.nchunks,
+                       D.lrows.as<LongRow>(), D.nlrows, part.as<Fr>(), C.stream);
     launch_from_mont(o + n, o, n, C.stream);
     std::vector<uint8_t> res(32 * n);
     SPX_HIP(hipMemcpyAsync(res.data(), o + n, 32 * n, hipMemcpyDeviceToHost, C.stream));

@@ -279,6 +279,12 @@ struct DevSparse {  // rank-local block of 3 matrices (CSR rows or CSC columns)
         return v;
     }
 };
+struct DevSliced {  // rank-local rows of A, B, C as the column-sorted entry list (kernels.hpp: SpmvSlicedView)
+    DevMem val, col, dst;
+    uint64_t entries = 0;
+    bool on = false;  // every local row of every matrix has at most one entry
+    SpmvSlicedView view() const { return SpmvSlicedView{val.as<Fr>(), col.as<uint32_t>(), dst.as<uint32_t>()}; }
+};
 struct DevColStream {  // rank-local columns of A, B, C for eval_on_x (kernels.hpp: ColStreamView)
     DevMem slices, lanes, rowm, val;
     uint32_t nslices = 0;
@@ -297,7 +303,8 @@ struct Index {
     int log_n = 0;
     uint64_t n = 0;
     HostCsr m[3];
-    DevSparse rows;      // local rows (SpMV)
+    DevSparse rows;      // local rows (SpMV), when rows_sliced is off
+    DevSliced rows_sliced;  // local rows as the column-sorted entry list (single-entry rows)
     DevColStream cols;   // local columns (eval_on_x)
     bool has_cache = false;
     Blake2s cache;  // transcript state after feeding A, B, C

@@ -60,7 +60,7 @@ C5_FILE = os.path.join(ROOT, "profiles", "r05", "r05d_c5_parity_2_24.json")
 MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
-KSYM = {"sc1_round": "k_sc1_wave<true, false, false>", "sc2_round": "k_sc2_wave<true, false, false>", "spmv3": "k_sparse3<0>",
+KSYM = {"sc1_round": "k_sc1_wave<true, false, false>", "sc2_round": "k_sc2_wave<true, false, false>", "spmv3": "k_spmv_sliced",
         "mtv3": "k_col_stream", "open_level": "k_open_fold_wave<3>", "eq_expand": "k_eq_expand", "msm_acc_g1": "k_accum_aff<Fq >",
         "msm_acc_g2": "k_accum_aff<Fq2>", "msm_accx_g1": "k_accum_xyzz<Fq >", "msm_accx_g2": "k_accum_xyzz<Fq2>"}
 KNAMES = ["sc1_round", "sc2_round", "spmv3", "mtv3", "open_level", "eq_expand", "msm_sort", "msm_acc_g1", "msm_acc_g2",
@@ -402,10 +402,14 @@ def largest_rate(d):
     return {"MB": round(mb, 2), "us": round(us, 2), "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-# BASELINE C2 (commitment stubbed): 16 proofs in flight. Its proofs are ~100x shorter than a full
-# proof's absorption and its kernels small: with 32 contexts on 4 hardware queues the index-cached C2
-# rate fell 843 -> 446 M (profiles/r04/r04ao_bench.json against r04af_bench.json)
-C2_INFLIGHT = 16
+# BASELINE C2 (commitment stubbed): its proofs are ~100x shorter than a full proof's absorption, so
+# the host's cores, not the GPU, set the per-proof-absorbed rate, and the runtime's spinning waits took
+# 13-15 of the 16 (profiles/r05/r05u_c2ab.jsonl). Its contexts poll their waits every 20 us
+# (C2_SYNC_POLL_US): 445 -> 525 M constraints/s at 16 in flight, 534-557 M at 32 (index-cached 746 ->
+# 783-794 M). 8 / 16 / 32 hardware queues instead of 4: 542-666 M index-cached (r05w_c2_hwq.jsonl).
+# (Round 4, spinning: 32 in flight on 4 queues had halved the index-cached rate against 16.)
+C2_INFLIGHT = 32
+C2_SYNC_POLL_US = 20
 
 
 def inflight_for(g):
@@ -670,6 +674,9 @@ def main():
         return cs, attach(cs, args.comm)
 
     ctxs = [spx.Context(device) for _ in range(Bb)] if need_batch else []
+    if stub:
+        for c in ctxs:
+            c.set_sync_poll(C2_SYNC_POLL_US)
     sctxs, hub = make_sharded(Bs) if need_sharded else ([], None)
     ctx = (ctxs or sctxs)[0]
     # the world size each rank's product communicator spans (one allgather of the rank ids on it)
@@ -1090,6 +1097,8 @@ def c2_line(spx, L, args, B):
     log_n, log_v, P = 18, args.log_v, 64
     n = 1 << log_n
     ctxs = [spx.Context(0) for _ in range(B)]
+    for c in ctxs:
+        c.set_sync_poll(C2_SYNC_POLL_US)
     syn, mats, zs, nnz = synth_instance(spx, 3, log_n, log_v, 0x5EED0000 + log_n, P, 0xB0B0)
     pk = spx.IndexPK(ctxs[0], index_from_c(spx, ctxs[0], mats), log_n)
     wits = [spx.Witness(ctxs[0], z[: 32 << log_v], z[32 << log_v :]) for z in zs]

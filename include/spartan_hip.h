@@ -128,6 +128,11 @@ int spx_ctx_set_lvl0_batch(spx_ctx *ctx, int mode);
  * recv receives world * bytes in rank order. For transport tests. */
 int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t bytes);
 
+/* How this context's host waits for its stream (no effect on the proof bytes): us > 0 polls an event
+ * every us microseconds (frees the host cores the HSA runtime's spinning wait would take: BASELINE C2
+ * with matrices absorbed per proof, sharded ranks), 0 = hipStreamSynchronize, -1 = the process default
+ * (SPX_SYNC_POLL_US, else 0). */
+int spx_ctx_set_sync_poll(spx_ctx *ctx, int us);
 /* free and total bytes of the context's device (hipMemGetInfo): bench.py sizes the proofs in flight
  * per rank from it (each context keeps grow-only scratch and an MSM workspace) */
 int spx_ctx_mem_info(spx_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);

@@ -94,6 +94,7 @@ EXPORTED = [
     "spx_ctx_comm_allgather",
     "spx_msm_reruns",
     "spx_ctx_mem_info",
+    "spx_ctx_set_sync_poll",
     "spx_host_phase_stats",
     "spx_pp_load",
     "spx_pp_generate",
@@ -171,6 +172,8 @@ def lib():
         L.spx_ctx_set_comm_rehearsal.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     if hasattr(L, "spx_msm_reruns") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_msm_reruns.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(L, "spx_ctx_set_sync_poll") or not os.environ.get("SPX_LIB_PATH"):
+        L.spx_ctx_set_sync_poll.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_ctx_mem_info") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_ctx_mem_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
@@ -342,6 +345,11 @@ class Context:
         out = ctypes.create_string_buffer(max(1, len(data) * world))
         _check(lib().spx_ctx_comm_allgather(self.h, data, out, len(data)))
         return [out.raw[k * len(data) : (k + 1) * len(data)] for k in range(world)]
+
+    def set_sync_poll(self, us):
+        """host waits of this context: poll an event every `us` microseconds (0: hipStreamSynchronize,
+        -1: the process default; spx_ctx_set_sync_poll)"""
+        _check(lib().spx_ctx_set_sync_poll(self.h, int(us)))
 
     def mem_info(self):
         """(free, total) bytes of this context's device (spx_ctx_mem_info)"""

@@ -608,6 +608,12 @@ int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
         if (ops) *ops = ctx->c->kprof.ops[id];
     });
 }
+int spx_ctx_set_sync_poll(spx_ctx* ctx, int us) {
+    return guard([&] {
+        if (!ctx) spx::invalid("null context");
+        ctx->c->poll_us = us < 0 ? -1 : us;
+    });
+}
 int spx_ctx_mem_info(spx_ctx* ctx, uint64_t* free_bytes, uint64_t* total_bytes) {
     return guard([&] {
         if (!free_bytes || !total_bytes) spx::invalid("null argument");

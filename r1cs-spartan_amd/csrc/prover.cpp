@@ -57,7 +57,7 @@ static int sync_poll_us() {
     return v;
 }
 void Ctx::wait_stream(hipStream_t s, hipEvent_t& ev) {
-    const int us = sync_poll_us();
+    const int us = poll_us >= 0 ? poll_us : sync_poll_us();
     if (us <= 0) {
         SPX_HIP(hipStreamSynchronize(s));
         return;
@@ -1072,8 +1072,11 @@ static OpenOut open_stub(Ctx& C, const Fr* z_local, int L, const std::vector<HFr
                    C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
     uint8_t* h = C.pin_at(Ctx::kPinOpen, 32 * (L + 1), 56 << 10);
     const Fr* rin = z_local;
-    for (int i = 0; i < nloc; ++i) {
-        Fr* rout = bufs[i & 1];
+    // z(point) only (no quotients): three levels per launch while the table is large, then the tail
+    // in one launch (level by level this was ~L launches per opening: C2's proofs are launch-bound)
+    int nb = 0;
+    for (int i = 0; i < nloc;) {
+        Fr* rout = bufs[nb++ & 1];
         const uint64_t half = nl >> (i + 1);
         if (open_tail_levels(half, nloc - i) == nloc - i) {  // the remaining levels in one launch
             std::vector<Fr> pts(nloc - i);
@@ -1082,8 +1085,17 @@ static OpenOut open_stub(Ctx& C, const Fr* z_local, int L, const std::vector<HFr
             rin = rout;
             break;
         }
-        launch_open_level(rin, rout, nullptr, dev_fr(point[i]), half, C.stream);
+        const int nf = nloc - i >= 3 && (half >> 2) >= 1 ? 3 : (nloc - i >= 2 && (half >> 1) >= 1 ? 2 : 1);
+        if (nf >= 2) {
+            Fr pts[3];
+            uint64_t qoffs[3] = {~0ull, ~0ull, ~0ull};
+            for (int j = 0; j < nf; ++j) pts[j] = dev_fr(point[i + j]);
+            launch_open_fold(rin, rout, nullptr, nf, pts, qoffs, nl >> (i + nf), C.stream);
+        } else {
+            launch_open_level(rin, rout, nullptr, dev_fr(point[i]), half, C.stream);
+        }
         rin = rout;
+        i += nf;
     }
     SPX_HIP(hipMemcpyAsync(h + 32 * L, rin, 32, hipMemcpyDeviceToHost, C.stream));
     C.sync();

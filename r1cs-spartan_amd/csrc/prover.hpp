@@ -202,6 +202,7 @@ struct Ctx {
     // rank and ~45 waits per proof that spinning was most of a proof's host CPU. With SPX_SYNC_POLL_US
     // = t > 0 the wait records an event and polls it, sleeping t us between polls (wait_stream).
     hipEvent_t wait_ev = nullptr, wait_ev_side = nullptr;
+    int poll_us = -1;  // this context's wait: -1 = SPX_SYNC_POLL_US (default 0), 0 = hipStreamSynchronize
     void wait_stream(hipStream_t s, hipEvent_t& ev);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
         wait_stream(stream, wait_ev);

@@ -566,6 +566,40 @@ def comm_seen(ctx, rank, world):
     return len(ids)
 
 
+def run_rehearsal(args, log_n, log_v, P):
+    """N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank (rank 0 of G) of every
+    proof, with no peers: every exchange returns its own contribution (spx_ctx_set_comm_rehearsal), so
+    the rank does a real rank's device and host work for its 1/G of the buckets, blocks and hashing.
+    Every rank of the node does the same on its own GPU, so the node's rate is this rank's proof rate
+    (exchange latency taken as free; the proofs of a rehearsal are not valid and are not checked).
+    Each G runs in a child process of its own (tools/vrank_bench.py --solo), with the settings an N = G
+    rank runs with: inflight_for(G) proofs in flight, lvl0_for(G), hw_queues_for(G) hardware queues and
+    sync_poll_for(G). The children run BEFORE this process creates its own contexts: their streams hold
+    hardware queues too, and 4 of this process's beside a child's 32 oversubscribed the GPU's queues
+    (a G = 8 child measured 377 M constraints/s beside them against 400-403 M alone,
+    profiles/r05/r05y_bench.json, r05z_steps.jsonl)."""
+    rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free), "
+                 "matrices absorbed per proof (1/G of them by this rank), in a child process "
+                 "(tools/vrank_bench.py --solo) run before the headline; node value = the rank's proof rate x n",
+                 "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "msm_reruns": {}, "device_memory": {}}
+    for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
+        env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues_for(G)))
+        env.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(G)))
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo",
+               "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P), "--steps", str(args.steps),
+               "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+        if r.returncode != 0:
+            raise RuntimeError("rehearsal G=%d failed: %s" % (G, r.stderr[-2000:]))
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        rehearsal["values"][str(G)] = d["node_estimate"]
+        rehearsal["proofs_in_flight"][str(G)] = d["inflight_per_rank"]
+        rehearsal["hw_queues"][str(G)] = hw_queues_for(G)
+        rehearsal["msm_reruns"][str(G)] = d["msm_reruns"]
+        rehearsal["device_memory"][str(G)] = d.get("device_memory")
+    return rehearsal
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -638,12 +672,14 @@ def main():
         os.environ.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(world)))
     else:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
-    spx = load_product()
-    L = spx.lib()
     Bb = args.inflight or (C2_INFLIGHT if stub else inflight_for(1))  # contexts of the unsharded (batch) proofs
     Bs = args.inflight or inflight_for(world)  # contexts of the proofs sharded over all ranks
     Bm = max(Bb, Bs, inflight_for(2))
     P = max(Bm, (args.proofs_per_step + Bm - 1) // Bm * Bm)  # proofs per step; each worker proves P / B of them
+    # the G-GPU rehearsals first, in child processes, while this process holds no GPU queue (run_rehearsal)
+    rehearsal = run_rehearsal(args, log_n, log_v, P) if world == 1 and args.rehearse and not stub else None
+    spx = load_product()
+    L = spx.lib()
     # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
     device = 0 if os.environ.get("SPX_BENCH_SAME_GPU") == "1" else local
     sharded_head = world > 1 and args.shard == "proof"
@@ -832,35 +868,6 @@ def main():
             check_batch(pgc, ref)
             grouped[K] = (elg, elgc)
             del gctxs, gpk
-
-    # ---- N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank (rank 0 of G) of every
-    # proof, with no peers: every exchange returns its own contribution (spx_ctx_set_comm_rehearsal), so
-    # the rank does a real rank's device and host work for its 1/G of the buckets, blocks and hashing.
-    # Every rank of the node does the same on its own GPU, so the node's rate is this rank's proof rate
-    # (exchange latency taken as free; the proofs of a rehearsal are not valid and are not checked).
-    # Each G runs in a child process of its own (tools/vrank_bench.py --solo), with the settings an N = G
-    # rank runs with: inflight_for(G) proofs in flight, lvl0_for(G), hw_queues_for(G) hardware queues
-    # (a process-wide HIP setting), and none of this process's contexts sharing its queues.
-    rehearsal = None
-    if world == 1 and args.rehearse and not stub:
-        rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free), "
-                     "matrices absorbed per proof (1/G of them by this rank), in a child process "
-                     "(tools/vrank_bench.py --solo); node value = the rank's proof rate x n",
-                     "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "msm_reruns": {}}
-        for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
-            env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues_for(G)))
-            env.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(G)))
-            cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo",
-                   "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P), "--steps", str(args.steps),
-                   "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
-            r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
-            if r.returncode != 0:
-                raise RuntimeError("rehearsal G=%d failed: %s" % (G, r.stderr[-2000:]))
-            d = json.loads(r.stdout.strip().splitlines()[-1])
-            rehearsal["values"][str(G)] = d["node_estimate"]
-            rehearsal["proofs_in_flight"][str(G)] = d["inflight_per_rank"]
-            rehearsal["hw_queues"][str(G)] = hw_queues_for(G)
-            rehearsal["msm_reruns"][str(G)] = d["msm_reruns"]
 
     ms = elapsed / args.steps * 1e3  # per step (P proofs)
     ms_c = elapsed_cached / args.steps * 1e3 if elapsed_cached else 0.0

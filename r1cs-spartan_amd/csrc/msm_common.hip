@@ -50,6 +50,13 @@ struct Digits {
         carry = v > half;
         return carry ? (int32_t)v - (int32_t)full : (int32_t)v;
     }
+    // c = 16 (every MSM of >= 2^14 points): window w is half-word w of the scalar, so nothing is
+    // shifted (w a constant in the unrolled loops); the same signed digits as next(16) in order
+    DEV int32_t at16(uint32_t w) {
+        const uint32_t v = ((s[w >> 1] >> (16 * (w & 1))) & 0xFFFFu) + carry;
+        carry = v > 0x8000u;
+        return carry ? (int32_t)v - 0x10000 : (int32_t)v;
+    }
 };
 // the digit's bucket if it is one of this rank's (local index in the batch), else ~0u
 DEV uint32_t digit_key(const MsmInst& I, int32_t d) {
@@ -105,7 +112,18 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
         // so the arrays are indexed statically); more windows recompute them in the writing pass
         constexpr uint32_t kKeep = 16;
         uint32_t cnt = 0, kkey[kKeep], kref[kKeep], kpos[kKeep];
-        if (live && I.W <= kKeep) {
+        if (live && I.c == 16 && I.W == kKeep) {
+            Digits d = d0;
+#pragma unroll
+            for (uint32_t w = 0; w < kKeep; ++w) {
+                const int32_t dg = d.at16(w);
+                kkey[w] = digit_key(I, dg);
+                kref[w] = digit_ref(I, w, j, dg);
+                cnt += kkey[w] != ~0u;
+                // independent returning atomics, issued back to back (their latency overlaps)
+                if constexpr (HIST) kpos[w] = kkey[w] != ~0u ? atomicAdd(&hist[kkey[w]], 1u) : 0u;
+            }
+        } else if (live && I.W <= kKeep) {
             Digits d = d0;
 #pragma unroll
             for (uint32_t w = 0; w < kKeep; ++w) {
@@ -116,7 +134,6 @@ __global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__
                     kref[w] = digit_ref(I, w, j, dg);
                 }
                 cnt += kkey[w] != ~0u;
-                // independent returning atomics, issued back to back (their latency overlaps)
                 if constexpr (HIST) kpos[w] = kkey[w] != ~0u ? atomicAdd(&hist[kkey[w]], 1u) : 0u;
             }
         } else if (live) {

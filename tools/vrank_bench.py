@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cached", action="store_true", help="index-cached matrix transcript")
+    ap.add_argument("--sync-dir", default="", help="side-by-side runs: wait (after the warm-up) until --sync-n "
+                    "processes have written a ready file into this directory, so their timed regions overlap")
+    ap.add_argument("--sync-n", type=int, default=1)
     ap.add_argument("--solo", action="store_true",
                     help="rehearsal: only rank 0 of the G, without peers (spx_ctx_set_comm_rehearsal), the GPU to "
                     "itself: value x G estimates an N = G node (exchanges free); its proofs are not valid")
@@ -90,13 +93,22 @@ def main():
 
     if a.warmup:
         run(a.warmup)
+    if a.sync_dir:
+        os.makedirs(a.sync_dir, exist_ok=True)
+        open(os.path.join(a.sync_dir, "ready.%d" % os.getpid()), "w").close()
+        t_wait = time.time()
+        while len([f for f in os.listdir(a.sync_dir) if f.startswith("ready.")]) < a.sync_n:
+            if time.time() - t_wait > 600:
+                raise SystemExit("side-by-side barrier timed out")
+            time.sleep(0.01)
     hp0 = spx.host_phase_stats()
     proofs, el, cpu = run(a.steps)
     hp1 = spx.host_phase_stats()
     npf = max(1, len(proofs))
     host_phases = {k: {"cpu_ms": round((hp1[k][0] - hp0[k][0]) / npf * 1e3, 3),
                        "wall_ms": round((hp1[k][1] - hp0[k][1]) / npf * 1e3, 3)} for k in hp1}
-    print(json.dumps({"G": world, "solo_rank0": a.solo, "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
+    t_end = time.time()
+    print(json.dumps({"G": world, "solo_rank0": a.solo, "t_start": round(t_end - el, 3), "t_end": round(t_end, 3), "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
                       "value": round(a.steps * P * n / el, 1), "ms_per_proof": round(el / (a.steps * P) * 1e3, 3),
                       # strong scaling: every rank works on every proof, so the node finishes the batch when
                       # rank 0 does (ranks are symmetric; exchanges taken as free)

@@ -408,8 +408,23 @@ def largest_rate(d):
 # (C2_SYNC_POLL_US): 445 -> 525 M constraints/s at 16 in flight, 534-557 M at 32 (index-cached 746 ->
 # 783-794 M). 8 / 16 / 32 hardware queues instead of 4: 542-666 M index-cached (r05w_c2_hwq.jsonl).
 # (Round 4, spinning: 32 in flight on 4 queues had halved the index-cached rate against 16.)
-C2_INFLIGHT = 32
+# Lockstep groups (spx_ctx_set_group, round 5): each context proves C2_GROUP proofs at a time, every
+# sumcheck round of the group one launch and one wait. One-at-a-time C2 proofs left the GPU idle 65%
+# of the time behind the 4 hardware queues (r05zg_c2_busy.txt); index-cached 790 M -> 1,166 M with 8
+# contexts x 4, 1,335 M with 8 x 8, 1,454 - 1,461 M with 16 x 8 (more queues: lower;
+# profiles/r05/r05zh_c2group.jsonl, r05zi_c2group.jsonl). C2_INFLIGHT counts proofs in flight.
+C2_INFLIGHT = 128
+C2_GROUP = 8
 C2_SYNC_POLL_US = 20
+
+
+def c2_contexts(spx, device, inflight):
+    """the C2 contexts: inflight / C2_GROUP lockstep groups, polling waits"""
+    cs = [spx.Context(device) for _ in range(max(1, inflight // C2_GROUP))]
+    for c in cs:
+        c.set_sync_poll(C2_SYNC_POLL_US)
+        c.set_group(C2_GROUP)
+    return cs
 
 
 def inflight_for(g):
@@ -672,7 +687,8 @@ def main():
         os.environ.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(world)))
     else:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(hw_queues_for(world)))
-    Bb = args.inflight or (C2_INFLIGHT if stub else inflight_for(1))  # contexts of the unsharded (batch) proofs
+    # contexts of the unsharded (batch) proofs (C2: one per lockstep group of C2_GROUP proofs)
+    Bb = max(1, (args.inflight or C2_INFLIGHT) // C2_GROUP) if stub else (args.inflight or inflight_for(1))
     Bs = args.inflight or inflight_for(world)  # contexts of the proofs sharded over all ranks
     Bm = max(Bb, Bs, inflight_for(2))
     P = max(Bm, (args.proofs_per_step + Bm - 1) // Bm * Bm)  # proofs per step; each worker proves P / B of them
@@ -709,10 +725,12 @@ def main():
             c.set_lvl0_batch(lvl0_for(world))
         return cs, attach(cs, args.comm)
 
-    ctxs = [spx.Context(device) for _ in range(Bb)] if need_batch else []
-    if stub:
-        for c in ctxs:
-            c.set_sync_poll(C2_SYNC_POLL_US)
+    if not need_batch:
+        ctxs = []
+    elif stub:
+        ctxs = c2_contexts(spx, device, Bb * C2_GROUP)
+    else:
+        ctxs = [spx.Context(device) for _ in range(Bb)]
     sctxs, hub = make_sharded(Bs) if need_sharded else ([], None)
     ctx = (ctxs or sctxs)[0]
     # the world size each rank's product communicator spans (one allgather of the rank ids on it)
@@ -937,7 +955,10 @@ def main():
         wl = "%s R1CS 2^%d constraints, |v|=%d, nnz=%d, %s, %s transcript, %s, %d proofs per step, %d in flight" % (
             KIND_NAMES.get(args.kind, str(args.kind)), log_n, 1 << log_v, nnz,
             "sumcheck-only, commitment stubbed (BASELINE C2)" if stub else "full prove + commit + 2 openings",
-            args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P, len(hctxs))
+            args.mode.upper(), ("one index, %d distinct witnesses" % W) if args.kind == 3 else "one witness", P,
+            len(hctxs) * (C2_GROUP if stub and not sharded_head else 1))
+        if stub and not sharded_head:
+            wl += " (%d lockstep groups of %d)" % (len(hctxs), C2_GROUP)
         out = {
             "metric": "R1CS constraints proved/sec at 2^%d%s" % (log_n, " (sumcheck-only, commitment stubbed)" if stub else ""),
             "value": round(jobs * n / (ms / 1e3), 1),
@@ -958,7 +979,8 @@ def main():
                 "baseline_config": "C2" if stub else "C3",
                 "distinct_witnesses": W,
                 "proofs_per_step": P,
-                "proofs_in_flight": len(hctxs),
+                "proofs_in_flight": len(hctxs) * (C2_GROUP if stub and not sharded_head else 1),
+                "lockstep_group": C2_GROUP if stub and not sharded_head else 1,
                 "parallelism": ("proof-sharded over %d ranks" % world) if sharded_head else ("%d independent ranks" % world),
                 "comm": args.comm if sctxs else None,
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or None,  # hardware queues per process
@@ -1103,9 +1125,7 @@ def c2_line(spx, L, args, B):
     same pipeline, its HBM-bound dominant kernel and the oracle's stubbed prover on all host cores."""
     log_n, log_v, P = 18, args.log_v, 64
     n = 1 << log_n
-    ctxs = [spx.Context(0) for _ in range(B)]
-    for c in ctxs:
-        c.set_sync_poll(C2_SYNC_POLL_US)
+    ctxs = c2_contexts(spx, 0, B)
     syn, mats, zs, nnz = synth_instance(spx, 3, log_n, log_v, 0x5EED0000 + log_n, P, 0xB0B0)
     pk = spx.IndexPK(ctxs[0], index_from_c(spx, ctxs[0], mats), log_n)
     wits = [spx.Witness(ctxs[0], z[: 32 << log_v], z[32 << log_v :]) for z in zs]
@@ -1139,8 +1159,8 @@ def c2_line(spx, L, args, B):
         "metric": "R1CS constraints proved/sec at 2^18 (sumcheck-only, commitment stubbed)",
         "value": round(steps * P * n / el, 1),
         "unit": "constraints/s",
-        "workload": "circuit-3n 2^18, |v|=%d, nnz=%d, %d distinct witnesses, FS transcript, %d in flight" % (
-            1 << log_v, nnz, P, B),
+        "workload": "circuit-3n 2^18, |v|=%d, nnz=%d, %d distinct witnesses, FS transcript, %d in flight "
+                    "(%d lockstep groups of %d)" % (1 << log_v, nnz, P, len(ctxs) * C2_GROUP, len(ctxs), C2_GROUP),
         "ms_per_proof_single_cached_transcript": round(el1 * 1e3, 3),
         "value_index_cached_transcript": round(steps * P * n / elc, 1),
         "kernels_ms_per_proof": {k: round(v["ms"], 4) for k, v in stats.items()},

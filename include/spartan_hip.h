@@ -133,6 +133,13 @@ int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t by
  * with matrices absorbed per proof, sharded ranks), 0 = hipStreamSynchronize, -1 = the process default
  * (SPX_SYNC_POLL_US, else 0). */
 int spx_ctx_set_sync_poll(spx_ctx *ctx, int us);
+/* Lockstep groups for spx_prove_many (no effect on the proof bytes): with k > 1 (at most 8) the
+ * context's stubbed-commitment proofs on an unsharded context (BASELINE C2) run k at a time in
+ * lockstep: each sumcheck round of the k proofs is one launch (blockIdx.y = proof) with one host wait,
+ * and the other steps queue the k proofs' launches before one wait. Other proofs, and
+ * k = 1 (the default), run one at a time. Replaces nothing in the reference (its prove is one proof,
+ * /root/reference/src/lib.rs:58-146); each proof's bytes are that prove's. */
+int spx_ctx_set_group(spx_ctx *ctx, int k);
 /* free and total bytes of the context's device (hipMemGetInfo): bench.py sizes the proofs in flight
  * per rank from it (each context keeps grow-only scratch and an MSM workspace) */
 int spx_ctx_mem_info(spx_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);

@@ -95,6 +95,7 @@ EXPORTED = [
     "spx_msm_reruns",
     "spx_ctx_mem_info",
     "spx_ctx_set_sync_poll",
+    "spx_ctx_set_group",
     "spx_host_phase_stats",
     "spx_pp_load",
     "spx_pp_generate",
@@ -174,6 +175,8 @@ def lib():
         L.spx_msm_reruns.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_sync_poll") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_ctx_set_sync_poll.argtypes = [vp, ctypes.c_int]
+    if hasattr(L, "spx_ctx_set_group") or not os.environ.get("SPX_LIB_PATH"):
+        L.spx_ctx_set_group.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_ctx_mem_info") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_ctx_mem_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
@@ -350,6 +353,11 @@ class Context:
         """host waits of this context: poll an event every `us` microseconds (0: hipStreamSynchronize,
         -1: the process default; spx_ctx_set_sync_poll)"""
         _check(lib().spx_ctx_set_sync_poll(self.h, int(us)))
+
+    def set_group(self, k):
+        """spx_prove_many runs this context's stubbed-commitment proofs k at a time in lockstep (one launch
+        per sumcheck round for the k proofs; 1 = one at a time; spx_ctx_set_group)"""
+        _check(lib().spx_ctx_set_group(self.h, int(k)))
 
     def mem_info(self):
         """(free, total) bytes of this context's device (spx_ctx_mem_info)"""

@@ -435,14 +435,17 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     int budget = (int)std::thread::hardware_concurrency();
     if (const char* e = getenv("OMP_NUM_THREADS")) budget = atoi(e);
     budget = std::max(1, budget);
-    const int nbase = std::min(nctx, G >= 4 ? std::max(1, budget / 2) : budget);
+    // proofs in flight: one per context, or its lockstep group (spx_ctx_set_group) for stubbed proofs
+    int nfly = 0;
+    for (int k = 0; k < nctx; ++k) nfly += (base.stub && G == 1) ? std::max(1, ctxs[k]->c->group) : 1;
+    const int nbase = std::min(nfly, G >= 4 ? std::max(1, budget / 2) : budget);
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
     // SPX_HASH_THREADS replaces the pool size (lead jobs included) and with it the scalar cap
     int nh_env = 0;
     if (const char* e = getenv("SPX_HASH_THREADS")) nh_env = std::max(1, atoi(e));
     const size_t nsize = nh_env ? (size_t)nh_env : (size_t)nbase + spx::HashSched::kLead;
-    spx::HashSched sched(owned.size(), (size_t)(nctx + G - 1) / G, lanes, base.stub ? 0 : 2,
+    spx::HashSched sched(owned.size(), (size_t)(nfly + G - 1) / G, lanes, base.stub ? 0 : 2,
                          2 * (size_t)(nh_env ? nh_env : nbase), nsize);
     const size_t njobs = sched.size();
     auto hasher = [&] {
@@ -477,26 +480,49 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
 
     std::vector<int> st(nctx, SPX_OK);
     std::vector<std::string> msg(nctx);
+    auto opts_for = [&](int i) {
+        spx::ProveOpts o = base;
+        o.seq = i;
+        if (!base.cached && i % G == rank)  // waited for inside prove, behind the proof's first kernels
+            o.await_absorbed = [&, i]() -> const spx::Blake2s* {
+                const auto w0 = clk::now();
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return slots[i].state.load() != 0; });
+                g_hash_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - w0).count();
+                if (slots[i].state.load() == 2)
+                    throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
+                return &slots[i].h;
+            };
+        return o;
+    };
+    auto emit = [&](int i, const std::vector<uint8_t>& p) {
+        if (p.size() > stride) spx::invalid("proof buffer too small");
+        memcpy(out + (size_t)i * stride, p.data(), p.size());
+        lens[i] = p.size();
+    };
     auto work = [&](int k) {
-        for (int i = k; i < nproofs; i += nctx) {
+        // lockstep groups (spx_ctx_set_group): the context's proofs k, k + nctx, ... in groups of K
+        const int K = ctxs[k]->c->group;
+        const bool grouped = K > 1 && base.stub && G == 1;
+        std::vector<int> mine;
+        for (int i = k; i < nproofs; i += nctx) mine.push_back(i);
+        for (size_t a = 0; a < mine.size(); a += grouped ? (size_t)K : 1) {
             int rc = guard([&] {
                 set_dev(ctxs[k]);
-                spx::ProveOpts o = base;
-                o.seq = i;
-                if (!base.cached && i % G == rank)  // waited for inside prove, behind the proof's first kernels
-                    o.await_absorbed = [&, i]() -> const spx::Blake2s* {
-                        const auto w0 = clk::now();
-                        std::unique_lock<std::mutex> lk(mu);
-                        cv.wait(lk, [&] { return slots[i].state.load() != 0; });
-                        g_hash_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - w0).count();
-                        if (slots[i].state.load() == 2)
-                            throw spx::SpxError(spx::kDevice, "absorption failed: " + pool_err);
-                        return &slots[i].h;
-                    };
-                auto p = spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, P, o);
-                if (p.size() > stride) spx::invalid("proof buffer too small");
-                memcpy(out + (size_t)i * stride, p.data(), p.size());
-                lens[i] = p.size();
+                if (!grouped) {
+                    const int i = mine[a];
+                    emit(i, spx::prove(*ctxs[k]->c, *idx->i, *wits[i]->w, P, opts_for(i)));
+                    return;
+                }
+                const int cnt = (int)std::min<size_t>((size_t)K, mine.size() - a);
+                std::vector<spx::ProveOpts> os;
+                std::vector<spx::Witness*> ws;
+                for (int q = 0; q < cnt; ++q) {
+                    os.push_back(opts_for(mine[a + q]));
+                    ws.push_back(wits[mine[a + q]]->w.get());
+                }
+                auto ps = spx::prove_group(*ctxs[k]->c, *idx->i, ws.data(), cnt, os.data());
+                for (int q = 0; q < cnt; ++q) emit(mine[a + q], ps[q]);
             });
             if (rc != SPX_OK) {
                 st[k] = rc;
@@ -612,6 +638,13 @@ int spx_ctx_set_sync_poll(spx_ctx* ctx, int us) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");
         ctx->c->poll_us = us < 0 ? -1 : us;
+    });
+}
+int spx_ctx_set_group(spx_ctx* ctx, int k) {
+    return guard([&] {
+        if (!ctx) spx::invalid("null context");
+        if (k < 1 || k > spx::kGroupMax) spx::invalid("lockstep group size must be 1.." + std::to_string(spx::kGroupMax));
+        ctx->c->group = k;
     });
 }
 int spx_ctx_mem_info(spx_ctx* ctx, uint64_t* free_bytes, uint64_t* total_bytes) {

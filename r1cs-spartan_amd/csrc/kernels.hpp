@@ -67,6 +67,36 @@ struct Tables3 {
     Fr* t[3];
 };
 
+// Lockstep groups (spx_ctx_set_group): one launch runs the same sumcheck round of up to kGroupMax
+// proofs of one index, proof j's blocks at blockIdx.y = j, each with its own tables, challenge,
+// partials, ticket and result (the per-proof launches' arguments, passed by value)
+static constexpr int kGroupMax = 8;
+struct Sc1Job {
+    Tables3 in, out;
+    const Fr* Ein;
+    Fr* Eout;
+    Fr r;
+    Fr* partial;  // kRoundPartials Fr of this proof
+    uint32_t* ticket;
+    Fr* result3;
+};
+struct Sc2Job {
+    const Fr* Min;
+    const Fr* Zin;
+    Fr* Mout;
+    Fr* Zout;
+    Fr r;
+    Fr* partial;
+    uint32_t* ticket;
+    Fr* result3;
+};
+struct Sc1Group {
+    Sc1Job j[kGroupMax];
+};
+struct Sc2Group {
+    Sc2Job j[kGroupMax];
+};
+
 // ---- live kernel statistics (HIP events around selected launches; off unless enabled)
 struct KProf {
     bool on = false;
@@ -183,6 +213,11 @@ void launch_sc1_round(bool fold, const Tables3& in, const Tables3& out, const Fr
                       uint64_t half, Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s);
 void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zout, const Fr& r, uint64_t half,
                       Fr* partial, uint32_t* ticket, Fr* result3, bool need1, hipStream_t s);
+// launch_sc1_round / launch_sc2_round for the k (<= kGroupMax) proofs of a lockstep group, in ONE launch
+// (and one reduction launch for large grids): the same kernels' arithmetic, so each proof's result3
+// equals its own launch's. need1 applies to every proof of the group.
+void launch_sc1_round_group(int k, bool fold, const Sc1Job* jobs, uint64_t half, bool need1, hipStream_t s);
+void launch_sc2_round_group(int k, bool fold, const Sc2Job* jobs, uint64_t half, bool need1, hipStream_t s);
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
 // the last levels of an opening in one launch: how many of the `remaining` levels starting at a level
 // of `half` pairs it takes (0: none), and the launch (points[j] folds level j; q receives the levels'

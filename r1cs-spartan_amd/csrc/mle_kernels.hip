@@ -72,6 +72,19 @@ __global__ __launch_bounds__(kThreads) void k_reduce_partials(const Fr* __restri
     }
     block_reduce_store<K>(acc, out);
 }
+// one block per proof of a lockstep group: proof blockIdx.x's partials into its result
+template <class Group>
+__global__ __launch_bounds__(kThreads) void k_reduce_partials_group(Group g, int nblk) {
+    const auto& j = g.j[blockIdx.x];
+    Fr acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fe_zero(acc[k]);
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fe_add(acc[k], acc[k], ld_fr(j.partial + (size_t)b * 3 + k));
+    }
+    block_reduce_store<3>(acc, j.result3);
+}
 
 // Last-block reduction (one launch per sumcheck round instead of two). The per-XCD L2s are not
 // coherent, and a __threadfence() per block (an L2 write-back + L1 invalidate, several us each) cost
@@ -564,10 +577,9 @@ DEV void fold2(Fr& x0, Fr& x1, const Fr* p, const Fr& r) {  // p[0..3] -> (p0 + 
     fe_add(x1, a2, d);
 }
 template <bool FUSED>
-__global__ __launch_bounds__(kThreads) void k_sc1_fold_quad(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
-                                                            Fr* __restrict__ Eout, const Fr r, uint64_t half,
-                                                            Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
-                                                            Fr* __restrict__ result3) {
+DEV void sc1_fold_quad_body(const Tables3& in, const Tables3& out, const Fr* __restrict__ Ein, Fr* __restrict__ Eout,
+                            const Fr& r, uint64_t half, Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                            Fr* __restrict__ result3) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -609,10 +621,22 @@ __global__ __launch_bounds__(kThreads) void k_sc1_fold_quad(Tables3 in, Tables3 
         block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
 }
 template <bool FUSED>
-__global__ __launch_bounds__(kThreads) void k_sc2_fold_pair(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
-                                                            Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
-                                                            uint64_t half, Fr* __restrict__ partial,
-                                                            uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+__global__ __launch_bounds__(kThreads) void k_sc1_fold_quad(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
+                                                            Fr* __restrict__ Eout, const Fr r, uint64_t half,
+                                                            Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                                                            Fr* __restrict__ result3) {
+    sc1_fold_quad_body<FUSED>(in, out, Ein, Eout, r, half, partial, ticket, result3);
+}
+// the same round of a lockstep group of proofs: proof blockIdx.y's job (its tables, challenge,
+// partials, ticket and result), gridDim.x blocks per proof
+__global__ __launch_bounds__(kThreads) void k_sc1_fold_quad_group(Sc1Group g, uint64_t half) {
+    const Sc1Job& j = g.j[blockIdx.y];
+    sc1_fold_quad_body<true>(j.in, j.out, j.Ein, j.Eout, j.r, half, j.partial, j.ticket, j.result3);
+}
+template <bool FUSED>
+DEV void sc2_fold_pair_body(const Fr* __restrict__ Min, const Fr* __restrict__ Zin, Fr* __restrict__ Mout,
+                            Fr* __restrict__ Zout, const Fr& r, uint64_t half, Fr* __restrict__ partial,
+                            uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
     Fr g[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) fe_zero(g[k]);
@@ -638,6 +662,17 @@ __global__ __launch_bounds__(kThreads) void k_sc2_fold_pair(const Fr* __restrict
         grid_reduce_last<3>(g, partial, ticket, result3);
     else
         block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+template <bool FUSED>
+__global__ __launch_bounds__(kThreads) void k_sc2_fold_pair(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
+                                                            Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
+                                                            uint64_t half, Fr* __restrict__ partial,
+                                                            uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+    sc2_fold_pair_body<FUSED>(Min, Zin, Mout, Zout, r, half, partial, ticket, result3);
+}
+__global__ __launch_bounds__(kThreads) void k_sc2_fold_pair_group(Sc2Group g, uint64_t half) {
+    const Sc2Job& j = g.j[blockIdx.y];
+    sc2_fold_pair_body<true>(j.Min, j.Zin, j.Mout, j.Zout, j.r, half, j.partial, j.ticket, j.result3);
 }
 
 // ------------------------------------------------------------------ wave-transposed fold rounds
@@ -748,10 +783,9 @@ DEV void wave_pair(const Fr* __restrict__ in, uint64_t base, uint4* lds, int lan
 // sumcheck #1 round (FOLD: round >= 2 with the fold of r_{i-1}; NEED1: also G(1)), one wave per 64
 // consecutive pairs (half a multiple of 64); the sums as k_sc1_round
 template <bool FOLD, bool NEED1, bool FUSED>
-__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
-                                                                   Fr* __restrict__ Eout, const Fr r, uint64_t half,
-                                                                   Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
-                                                                   Fr* __restrict__ result3) {
+DEV void sc1_wave_body(const Tables3& in, const Tables3& out, const Fr* __restrict__ Ein, Fr* __restrict__ Eout,
+                       const Fr& r, uint64_t half, Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                       Fr* __restrict__ result3) {
     __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
     uint4* lds = lds_all[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
@@ -807,13 +841,24 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, 
     else
         block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
 }
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave(Tables3 in, Tables3 out, const Fr* __restrict__ Ein,
+                                                                   Fr* __restrict__ Eout, const Fr r, uint64_t half,
+                                                                   Fr* __restrict__ partial, uint32_t* __restrict__ ticket,
+                                                                   Fr* __restrict__ result3) {
+    sc1_wave_body<FOLD, NEED1, FUSED>(in, out, Ein, Eout, r, half, partial, ticket, result3);
+}
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc1_wave_group(Sc1Group g, uint64_t half) {
+    const Sc1Job& j = g.j[blockIdx.y];
+    sc1_wave_body<FOLD, NEED1, FUSED>(j.in, j.out, j.Ein, j.Eout, j.r, half, j.partial, j.ticket, j.result3);
+}
 
 // sumcheck #2 round, one wave per 64 consecutive pairs; the sums as k_sc2_round
 template <bool FOLD, bool NEED1, bool FUSED>
-__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
-                                                                   Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
-                                                                   uint64_t half, Fr* __restrict__ partial,
-                                                                   uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+DEV void sc2_wave_body(const Fr* __restrict__ Min, const Fr* __restrict__ Zin, Fr* __restrict__ Mout,
+                       Fr* __restrict__ Zout, const Fr& r, uint64_t half, Fr* __restrict__ partial,
+                       uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
     __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
     uint4* lds = lds_all[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
@@ -851,6 +896,18 @@ __global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __
         grid_reduce_last<3>(g, partial, ticket, result3);
     else
         block_reduce_store<3>(g, partial + (size_t)blockIdx.x * 3);
+}
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave(const Fr* __restrict__ Min, const Fr* __restrict__ Zin,
+                                                                   Fr* __restrict__ Mout, Fr* __restrict__ Zout, const Fr r,
+                                                                   uint64_t half, Fr* __restrict__ partial,
+                                                                   uint32_t* __restrict__ ticket, Fr* __restrict__ result3) {
+    sc2_wave_body<FOLD, NEED1, FUSED>(Min, Zin, Mout, Zout, r, half, partial, ticket, result3);
+}
+template <bool FOLD, bool NEED1, bool FUSED>
+__global__ __launch_bounds__(kThreads) SPX_WAVE_OCC void k_sc2_wave_group(Sc2Group g, uint64_t half) {
+    const Sc2Job& j = g.j[blockIdx.y];
+    sc2_wave_body<FOLD, NEED1, FUSED>(j.Min, j.Zin, j.Mout, j.Zout, j.r, half, j.partial, j.ticket, j.result3);
 }
 
 // ------------------------------------------------------------------ sumcheck #2 round
@@ -1274,6 +1331,87 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
         sc2_launch<false>(g, Min, Zin, Mout, Zout, r, half, partial, ticket, result3, need1 ? 1 : 0, s);
     kp_end(32.0 * (double)half * (fold ? 12.0 : 4.0), s);
     if (g > kFuseMaxBlocks) hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kThreads), 0, s, partial, g, result3);
+}
+
+// ---- lockstep groups: the launch decisions of launch_sc1_round / launch_sc2_round, one launch for k
+// proofs (grid gridDim.x per proof, blockIdx.y = proof). Round shapes without a group kernel (small
+// rounds that need G(1), or a round 1 below kWaveMinHalf) launch per proof.
+template <class Group, class Job>
+static Group group_of(int k, const Job* jobs) {
+    if (k < 1 || k > kGroupMax) throw std::invalid_argument("lockstep group size out of range");
+    Group g{};
+    for (int i = 0; i < k; ++i) g.j[i] = jobs[i];
+    return g;
+}
+template <bool FOLD, bool NEED1>
+static void sc1_wave_group_launch(int k, int g, const Sc1Group& G, uint64_t half, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc1_wave_group<FOLD, NEED1, true>), dim3(g, k), dim3(kThreads), 0, s, G, half);
+    else
+        hipLaunchKernelGGL((k_sc1_wave_group<FOLD, NEED1, false>), dim3(g, k), dim3(kThreads), 0, s, G, half);
+}
+template <bool FOLD, bool NEED1>
+static void sc2_wave_group_launch(int k, int g, const Sc2Group& G, uint64_t half, hipStream_t s) {
+    if (g <= kFuseMaxBlocks)
+        hipLaunchKernelGGL((k_sc2_wave_group<FOLD, NEED1, true>), dim3(g, k), dim3(kThreads), 0, s, G, half);
+    else
+        hipLaunchKernelGGL((k_sc2_wave_group<FOLD, NEED1, false>), dim3(g, k), dim3(kThreads), 0, s, G, half);
+}
+void launch_sc1_round_group(int k, bool fold, const Sc1Job* jobs, uint64_t half, bool need1, hipStream_t s) {
+    const Sc1Group G = group_of<Sc1Group>(k, jobs);
+    if (half < kWaveMinHalf && !(fold && !need1)) {
+        for (int i = 0; i < k; ++i)
+            launch_sc1_round(fold, jobs[i].in, jobs[i].out, jobs[i].Ein, jobs[i].Eout, jobs[i].r, half, jobs[i].partial,
+                             jobs[i].ticket, jobs[i].result3, need1, s);
+        return;
+    }
+    int g;
+    kp_begin(KP_SC1, s);
+    if (half >= kWaveMinHalf) {
+        g = grid_for(half, kWaveMaxBlocks);
+        if (fold && need1)
+            sc1_wave_group_launch<true, true>(k, g, G, half, s);
+        else if (fold)
+            sc1_wave_group_launch<true, false>(k, g, G, half, s);
+        else if (need1)
+            sc1_wave_group_launch<false, true>(k, g, G, half, s);
+        else
+            sc1_wave_group_launch<false, false>(k, g, G, half, s);
+    } else {  // small fold round without G(1)
+        g = grid_for(4 * half, kFuseMaxBlocks);
+        hipLaunchKernelGGL(k_sc1_fold_quad_group, dim3(g, k), dim3(kThreads), 0, s, G, half);
+    }
+    kp_end(32.0 * (double)k * (double)half * (fold ? (14.0 + 6.0 + (jobs[0].Eout ? 1.0 : 0.0)) : 7.0), s);
+    if (g > kFuseMaxBlocks)
+        hipLaunchKernelGGL(k_reduce_partials_group<Sc1Group>, dim3(k), dim3(kThreads), 0, s, G, g);
+}
+void launch_sc2_round_group(int k, bool fold, const Sc2Job* jobs, uint64_t half, bool need1, hipStream_t s) {
+    const Sc2Group G = group_of<Sc2Group>(k, jobs);
+    if (half < kWaveMinHalf && !(fold && !need1)) {
+        for (int i = 0; i < k; ++i)
+            launch_sc2_round(fold, jobs[i].Min, jobs[i].Zin, jobs[i].Mout, jobs[i].Zout, jobs[i].r, half, jobs[i].partial,
+                             jobs[i].ticket, jobs[i].result3, need1, s);
+        return;
+    }
+    int g;
+    kp_begin(KP_SC2, s);
+    if (half >= kWaveMinHalf) {
+        g = grid_for(half, kWaveMaxBlocks);
+        if (fold && need1)
+            sc2_wave_group_launch<true, true>(k, g, G, half, s);
+        else if (fold)
+            sc2_wave_group_launch<true, false>(k, g, G, half, s);
+        else if (need1)
+            sc2_wave_group_launch<false, true>(k, g, G, half, s);
+        else
+            sc2_wave_group_launch<false, false>(k, g, G, half, s);
+    } else {  // small fold round without P(1)
+        g = grid_for(2 * half, kFuseMaxBlocks);
+        hipLaunchKernelGGL(k_sc2_fold_pair_group, dim3(g, k), dim3(kThreads), 0, s, G, half);
+    }
+    kp_end(32.0 * (double)k * (double)half * (fold ? 12.0 : 4.0), s);
+    if (g > kFuseMaxBlocks)
+        hipLaunchKernelGGL(k_reduce_partials_group<Sc2Group>, dim3(k), dim3(kThreads), 0, s, G, g);
 }
 
 int open_tail_levels(uint64_t half, int remaining) {

@@ -1564,6 +1564,338 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     return proof.b;
 }
 
+// ====================================================================== lockstep groups
+// prove() for k stubbed-commitment proofs of one index on one rank (BASELINE C2), interleaved step by
+// step. A C2 proof is ~55 small launches and ~40 host waits: with 32 proofs in flight on the context
+// streams' 4 hardware queues the GPU ran ~1 kernel at a time and was idle 65% of the time (trace
+// profiles/r05/r05zg_c2_busy.txt), each proof waiting its turn in a queue. Here the k proofs' sumcheck
+// rounds are one launch each (launch_sc1_round_group: blockIdx.y = proof) with one wait, and the other
+// steps queue the k proofs' launches back to back before one wait. Every value is computed by the same
+// kernels and host formulas as prove(), so each proof's bytes are its own prove()'s.
+std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* Ws, int k, const ProveOpts* os) {
+    if (k < 1 || k > kGroupMax) invalid("lockstep group size must be 1.." + std::to_string(kGroupMax));
+    CtxClaim claim;
+    claim.take(C);
+    struct UnwindDrain {
+        Ctx& C;
+        int pending = std::uncaught_exceptions();
+        ~UnwindDrain() {
+            if (std::uncaught_exceptions() <= pending) return;
+            (void)hipStreamSynchronize(C.stream);
+        }
+    } drain{C};
+    Comm& comm = *C.comm;
+    if (comm.size() != 1 || I.G != 1) invalid("lockstep groups need an unsharded context and index");
+    const int L = I.log_n;
+    const uint64_t n = I.n, nl = n;
+    for (int j = 0; j < k; ++j) {
+        if (!Ws[j]) invalid("null witness");
+        if (!os[j].stub || os[j].coins || os[j].claimed) invalid("lockstep groups prove stubbed-commitment proofs only");
+        if (!is_pow2(Ws[j]->v.size() / 32)) invalid("public input should be power of two");
+        if (Ws[j]->n != n) invalid("|v| + |w| != number of variables");  // prover.rs:117-119
+    }
+    const bool check_derived = [] {
+        const char* e = getenv("SPX_CHECK_DERIVED");
+        return e && e[0] == '1';
+    }();
+    // per-proof scratch, prove()'s layout at G = 1
+    const uint64_t n2 = std::max<uint64_t>(nl / 2, 1), n4 = std::max<uint64_t>(nl / 4, 1);
+    const uint64_t npart = std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks));
+    const uint64_t need = 3 * nl + 3 * n2 + 3 * n4 + n2 + n4 + std::max<uint64_t>(nl / 8, 1) + nl + n2 + n4 + n2 + n4 +
+                          npart + 8192 * 2 + kEqScratch + 64 + 8 * L;
+    C.scratch.ensure(32 * need * (uint64_t)k);
+    static_assert(kGroupMax * 8192 <= (64 << 10), "per-proof pinned regions");
+    if (32 * (L + 3) > 4096 || 32 * (L + 1) > 2048) invalid("log_n too large for a lockstep group");
+    uint8_t* hp0 = C.pin_at(Ctx::kPinHp, kGroupMax * 8192, 64 << 10);
+    uint8_t* ho0 = C.pin_at(Ctx::kPinOpen, kGroupMax * 2048, 56 << 10);
+    struct P {
+        Fr *Az, *Bz, *Cz, *F1[3], *F2[3], *E1, *Ea, *Eb, *M0, *M1, *M2, *Z1, *Z2, *partial, *eqlo, *eqhi, *eqf, *chdev;
+        uint8_t *hp, *ho;
+        Fr* res_dev;
+        const Fr* z;
+        int log_v;
+        Transcript T;
+        Ser proof;
+        std::vector<HFr> tau, r_x, r_y;
+        HFr Cc, claim1, claim2;
+        Tables3 cur;
+        const Fr* Ecur;
+        const Fr *Mc, *Zc;
+    };
+    std::vector<P> ps;
+    ps.reserve(k);
+    for (int j = 0; j < k; ++j) {
+        Fr* base = C.scratch.as<Fr>() + need * j;
+        uint64_t off = 0;
+        auto take = [&](uint64_t c) {
+            Fr* q = base + off;
+            off += c;
+            return q;
+        };
+        P p;
+        p.Az = take(nl), p.Bz = take(nl), p.Cz = take(nl);
+        for (int m = 0; m < 3; ++m) p.F1[m] = take(n2);
+        for (int m = 0; m < 3; ++m) p.F2[m] = take(n4);
+        p.E1 = take(n2), p.Ea = take(n4), p.Eb = take(std::max<uint64_t>(nl / 8, 1));
+        p.M0 = take(nl), p.M1 = take(n2), p.M2 = take(n4);
+        p.Z1 = take(n2), p.Z2 = take(n4);
+        p.partial = take(npart);
+        p.eqlo = take(8192), p.eqhi = take(8192), p.eqf = take(kEqScratch);
+        p.chdev = take(8 * L);
+        p.hp = hp0 + 8192 * j;
+        p.ho = ho0 + 2048 * j;
+        p.res_dev = C.pin_dev<Fr>(p.hp);
+        p.z = Ws[j]->z.as<Fr>();
+        p.log_v = ilog2(Ws[j]->v.size() / 32);
+        p.T = Transcript(os[j].mode == 1, os[j].seed, nullptr);
+        ps.push_back(std::move(p));
+    }
+    // ---- SpMV Az, Bz, Cz of every proof (challenge-independent)
+    for (auto& p : ps) {
+        kp_begin(KP_SPMV, C.stream);
+        if (I.rows_sliced.on)
+            launch_spmv_sliced(I.rows_sliced.view(), p.z, p.Az, p.Bz, p.Cz, I.rows_sliced.entries, C.stream);
+        else
+            launch_sparse3(0, I.rows.view(), p.z, p.Az, p.Bz, p.Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(),
+                           I.rows.nchunks, I.rows.lrows.as<LongRow>(), I.rows.nlrows, p.partial, C.stream);
+        kp_end(I.rows_bytes, C.stream);
+    }
+    // ---- transcripts: A, B, C (cached or absorbed), v; round 1 with the stubbed commitment
+    for (int j = 0; j < k; ++j) {
+        P& p = ps[j];
+        const ProveOpts& o = os[j];
+        C.prove_seq++;
+        if (o.cached && I.has_cache)
+            p.T.set_state(I.cache);
+        else {
+            const Blake2s* absorbed = o.await_absorbed ? o.await_absorbed() : o.absorbed;
+            p.T.set_state(absorbed ? *absorbed : absorb_matrices(I));
+        }
+        Ser s;
+        s.u64(Ws[j]->v.size() / 32);
+        s.raw(Ws[j]->v.data(), Ws[j]->v.size());
+        p.T.absorb(s.b.data(), s.b.size());
+        const Affine<HFq> com{HFq::zero(), HFq::zero(), true};
+        p.proof.u64((uint64_t)L);
+        uint8_t b[48];
+        host::g1_compress(b, com);
+        p.proof.raw(b, 48);
+        p.T.feed(p.proof.b.data(), p.proof.b.size());
+    }
+    // stubbed openings of every proof's z (open_stub's launches; the chains share the fold buffers, in
+    // stream order) and one wait
+    Fr* obuf[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
+                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
+    auto open_all = [&](const std::vector<std::vector<HFr>>& pts) {
+        for (int j = 0; j < k; ++j) {
+            const std::vector<HFr>& point = pts[j];
+            const Fr* rin = ps[j].z;
+            int nb = 0;
+            for (int i = 0; i < L;) {
+                Fr* rout = obuf[nb++ & 1];
+                const uint64_t half = nl >> (i + 1);
+                if (open_tail_levels(half, L - i) == L - i) {
+                    std::vector<Fr> tp(L - i);
+                    for (int q = i; q < L; ++q) tp[q - i] = dev_fr(point[q]);
+                    launch_open_tail(rin, nullptr, half, L - i, tp.data(), rout, C.stream);
+                    rin = rout;
+                    break;
+                }
+                const int nf = L - i >= 3 && (half >> 2) >= 1 ? 3 : (L - i >= 2 && (half >> 1) >= 1 ? 2 : 1);
+                if (nf >= 2) {
+                    Fr fp[3];
+                    uint64_t qoffs[3] = {~0ull, ~0ull, ~0ull};
+                    for (int q = 0; q < nf; ++q) fp[q] = dev_fr(point[i + q]);
+                    launch_open_fold(rin, rout, nullptr, nf, fp, qoffs, nl >> (i + nf), C.stream);
+                } else {
+                    launch_open_level(rin, rout, nullptr, dev_fr(point[i]), half, C.stream);
+                }
+                rin = rout;
+                i += nf;
+            }
+            SPX_HIP(hipMemcpyAsync(ps[j].ho, rin, 32, hipMemcpyDeviceToHost, C.stream));
+        }
+        C.sync();
+        const std::vector<Affine<HFq2>> none(L, Affine<HFq2>{HFq2::zero(), HFq2::zero(), true});
+        for (int j = 0; j < k; ++j) {
+            P& p = ps[j];
+            const size_t m0 = p.proof.b.size();
+            ser_open(p.proof, ld_hfr(p.ho), h_of(nullptr), none);
+            p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+        }
+    };
+    {  // round 2: open at (r_v, 0...0)
+        std::vector<std::vector<HFr>> pts(k);
+        for (int j = 0; j < k; ++j) {
+            pts[j].assign(L, HFr::zero());
+            for (int i = 0; i < ps[j].log_v; ++i) pts[j][i] = ps[j].T.rand_fr();
+        }
+        open_all(pts);
+    }
+    // ---- round 3: tau, eq table; sumcheck 1 setup
+    for (auto& p : ps) {
+        p.tau.resize(L);
+        for (int i = 0; i < L; ++i) p.tau[i] = p.T.rand_fr();
+        memcpy(p.hp, p.tau.data(), 32 * L);
+        SPX_HIP(hipMemcpyAsync(p.chdev, p.hp, 32 * L, hipMemcpyHostToDevice, C.stream));
+        if (L >= 2)
+            launch_eq_table(p.chdev + 1, L - 1, 0, nl / 2, p.E1, p.eqlo, p.eqhi, C.stream);
+        else {
+            const HFr one = HFr::one();
+            memcpy(p.hp + 4096, &one, 32);
+            SPX_HIP(hipMemcpyAsync(p.E1, p.hp + 4096, 32, hipMemcpyHostToDevice, C.stream));
+        }
+        const size_t m0 = p.proof.b.size();
+        p.proof.u64((uint64_t)(L + 2));
+        p.proof.u64((uint64_t)L);
+        p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+        p.proof.u64((uint64_t)L);
+        p.Cc = HFr::one();
+        p.claim1 = HFr::zero();
+        p.cur = Tables3{{p.Az, p.Bz, p.Cz}};
+        p.Ecur = p.E1;
+    }
+    // ---- sumcheck 1: one launch and one wait per round for the group
+    std::vector<Sc1Job> j1(k);
+    std::vector<char> derive(k);
+    for (int i = 1; i <= L; ++i) {
+        const uint64_t half = nl >> i;
+        const bool fold = i >= 2;
+        bool need1 = check_derived;
+        for (int j = 0; j < k; ++j) {
+            P& p = ps[j];
+            Sc1Job& jb = j1[j];
+            jb.in = p.cur;
+            jb.out = Tables3{{nullptr, nullptr, nullptr}};
+            jb.Ein = p.Ecur;
+            jb.Eout = nullptr;
+            if (fold) {
+                Fr** fb = (i % 2 == 0) ? p.F1 : p.F2;
+                jb.out = Tables3{{fb[0], fb[1], fb[2]}};
+                if (i < L) jb.Eout = (i & 1) ? p.Eb : p.Ea;
+            }
+            jb.r = fold ? dev_fr(p.r_x[i - 2]) : Fr{};
+            jb.partial = p.partial;
+            jb.ticket = C.ticket + j;
+            jb.result3 = p.res_dev;
+            const HFr ct = p.Cc * p.tau[i - 1];
+            derive[j] = fold && !ct.is_zero();
+            need1 = need1 || !derive[j];
+        }
+        launch_sc1_round_group(k, fold, j1.data(), half, need1, C.stream);
+        C.sync();
+        for (int j = 0; j < k; ++j) {
+            P& p = ps[j];
+            HFr gs[3] = {ld_hfr(p.hp), ld_hfr(p.hp + 32), ld_hfr(p.hp + 64)};
+            const HFr ct = p.Cc * p.tau[i - 1];
+            if (derive[j]) {
+                const HFr d1 = (p.claim1 - (p.Cc - ct) * gs[0]) * ct.inv();
+                if (check_derived && !(d1 == gs[1]))
+                    throw SpxError(kSumcheck, "sumcheck 1 round " + std::to_string(i) + ": derived G(1) differs from the device's");
+                gs[1] = d1;
+            }
+            std::vector<HFr> msg = sc1_message(p.Cc, p.tau[i - 1], gs, L);
+            const size_t m0 = p.proof.b.size();
+            p.proof.u64(msg.size());
+            for (auto& e : msg) p.proof.fr(e);
+            p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+            const HFr ch = p.T.rand_fr();
+            p.r_x.push_back(ch);
+            const HFr eqc = eq1(p.tau[i - 1], ch);
+            p.claim1 = p.Cc * eqc * quad_at(gs, ch);
+            p.Cc = p.Cc * eqc;
+            if (fold) {
+                p.cur = j1[j].out;
+                if (j1[j].Eout) p.Ecur = j1[j].Eout;
+            }
+        }
+    }
+    // the tables hold 2 entries each: bind r_L on the host (prove()'s G = 1 case)
+    for (auto& p : ps)
+        for (int m = 0; m < 3; ++m) SPX_HIP(hipMemcpyAsync(p.hp + 64 * m, p.cur.t[m], 64, hipMemcpyDeviceToHost, C.stream));
+    C.sync();
+    for (auto& p : ps) {
+        const HFr r = p.r_x.back();
+        HFr v[3];
+        for (int m = 0; m < 3; ++m) {
+            const HFr a0 = ld_hfr(p.hp + 64 * m), a1 = ld_hfr(p.hp + 64 * m + 32);
+            v[m] = a0 + r * (a1 - a0);
+        }
+        // ---- round 4
+        size_t m0 = p.proof.b.size();
+        for (int m = 0; m < 3; ++m) p.proof.fr(v[m]);
+        p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+        HFr rabc[3] = {p.T.rand_fr(), p.T.rand_fr(), p.T.rand_fr()};
+        // ---- round 5: M_rx (the previous wait covers the staging region's earlier copies)
+        Fr* rxdev = p.chdev + 2 * L;
+        memcpy(p.hp + 256, p.r_x.data(), 32 * L);
+        memcpy(p.hp + 256 + 32 * L, rabc, 96);
+        SPX_HIP(hipMemcpyAsync(rxdev, p.hp + 256, 32 * (L + 3), hipMemcpyHostToDevice, C.stream));
+        kp_begin(KP_MTV, C.stream);
+        I.cols.launch(rxdev, L, rxdev + L, p.M0, p.eqf, p.partial, C.stream);
+        kp_end(I.cols_bytes, C.stream);
+        m0 = p.proof.b.size();
+        p.proof.u64(2);
+        p.proof.u64((uint64_t)L);
+        p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+        p.proof.u64((uint64_t)L);
+        p.claim2 = HFr::zero();
+        p.Mc = p.M0;
+        p.Zc = p.z;
+    }
+    // ---- sumcheck 2
+    std::vector<Sc2Job> j2(k);
+    for (int i = 1; i <= L; ++i) {
+        const uint64_t half = nl >> i;
+        const bool fold = i >= 2;
+        for (int j = 0; j < k; ++j) {
+            P& p = ps[j];
+            Sc2Job& jb = j2[j];
+            jb.Min = p.Mc;
+            jb.Zin = p.Zc;
+            jb.Mout = fold ? ((i & 1) ? p.M2 : p.M1) : nullptr;
+            jb.Zout = fold ? ((i & 1) ? p.Z2 : p.Z1) : nullptr;
+            jb.r = fold ? dev_fr(p.r_y[i - 2]) : Fr{};
+            jb.partial = p.partial;
+            jb.ticket = C.ticket + j;
+            jb.result3 = p.res_dev;
+        }
+        // (round 5's copies out of hp + 256 are ordered before this round's results land in hp)
+        launch_sc2_round_group(k, fold, j2.data(), half, !fold || check_derived, C.stream);
+        C.sync();
+        for (int j = 0; j < k; ++j) {
+            P& p = ps[j];
+            HFr q[3] = {ld_hfr(p.hp), ld_hfr(p.hp + 32), ld_hfr(p.hp + 64)};
+            if (fold) {
+                const HFr d1 = p.claim2 - q[0];
+                if (check_derived && !(d1 == q[1]))
+                    throw SpxError(kSumcheck, "sumcheck 2 round " + std::to_string(i) + ": derived P(1) differs from the device's");
+                q[1] = d1;
+            }
+            const size_t m0 = p.proof.b.size();
+            p.proof.u64(3);
+            for (int t = 0; t < 3; ++t) p.proof.fr(q[t]);
+            p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
+            const HFr ch = p.T.rand_fr();
+            p.r_y.push_back(ch);
+            p.claim2 = quad_at(q, ch);
+            if (fold) {
+                p.Mc = j2[j].Mout;
+                p.Zc = j2[j].Zout;
+            }
+        }
+    }
+    // ---- round 6: open at r_y
+    {
+        std::vector<std::vector<HFr>> pts(k);
+        for (int j = 0; j < k; ++j) pts[j] = ps[j].r_y;
+        open_all(pts);
+    }
+    std::vector<std::vector<uint8_t>> out(k);
+    for (int j = 0; j < k; ++j) out[j] = std::move(ps[j].proof.b);
+    return out;
+}
+
 // ====================================================================== kernel-level entry points
 // ====================================================================== verifier
 // lib.rs:147-212 with verifier.rs:143-512. The transcript is replayed on the host; the O(nnz) matrix

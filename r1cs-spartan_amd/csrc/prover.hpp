@@ -203,6 +203,9 @@ struct Ctx {
     // = t > 0 the wait records an event and polls it, sleeping t us between polls (wait_stream).
     hipEvent_t wait_ev = nullptr, wait_ev_side = nullptr;
     int poll_us = -1;  // this context's wait: -1 = SPX_SYNC_POLL_US (default 0), 0 = hipStreamSynchronize
+    // spx_prove_many on this context proves its stubbed-commitment, unsharded proofs in lockstep groups
+    // of this many (prove_group; 1 = one at a time)
+    int group = 1;
     void wait_stream(hipStream_t s, hipEvent_t& ev);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
         wait_stream(stream, wait_ev);
@@ -352,6 +355,11 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats);
 std::unique_ptr<Witness> witness_upload(Ctx& C, const uint8_t* v, size_t nv, const uint8_t* w, size_t nw);
 // P may be null only when o.stub
 std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts& o);
+// k (<= kGroupMax) proofs of one index in lockstep (BASELINE C2's form: commitment stubbed, one rank):
+// the same steps as prove() for each, with every sumcheck round of the k proofs in one launch and one
+// host wait, and the other steps' launches of the k proofs queued back to back before one wait. Each
+// proof's bytes equal its own prove()'s; o[j] are proof j's options (all stubbed, none interactive).
+std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* W, int k, const ProveOpts* o);
 size_t proof_size(int log_n);
 
 // verifier (lib.rs:147-212 with verifier.rs:143-512); VerifierParameter: data_structures.rs:19-26

@@ -218,6 +218,23 @@ void launch_sc2_round(bool fold, const Fr* Min, const Fr* Zin, Fr* Mout, Fr* Zou
 // equals its own launch's. need1 applies to every proof of the group.
 void launch_sc1_round_group(int k, bool fold, const Sc1Job* jobs, uint64_t half, bool need1, hipStream_t s);
 void launch_sc2_round_group(int k, bool fold, const Sc2Job* jobs, uint64_t half, bool need1, hipStream_t s);
+// the other steps of a lockstep group, one launch per step for the k proofs (each proof's arguments as
+// its own launch would take them; outputs bit-identical to the per-proof launchers):
+// SpMV over the column-sorted entry list into out[j] = (Az, Bz, Cz);
+void launch_spmv_sliced_group(int k, const SpmvSlicedView& v, const Fr* const* z, const Tables3* out, uint64_t entries,
+                              hipStream_t s);
+// launch_eq_table per proof (nvar variables at r_dev[j], scratch tables lo[j], hi[j]);
+void launch_eq_table_group(int k, const Fr* const* r_dev, int nvar, uint64_t base, uint64_t count, Fr* const* out,
+                           Fr* const* lo, Fr* const* hi, hipStream_t s);
+// launch_col_stream per proof, for an index without long columns (the caller checks);
+void launch_col_stream_group(int k, const ColStreamView& cv, const Fr* const* r_x, int L, const Fr* const* scale,
+                             Fr* const* out, Fr* const* eq_scratch, hipStream_t s);
+// z_j(points_j) by the stubbed opening's fold chain (no quotients), the value written to last[j]
+// (host-mapped pinned memory allowed); bufA / bufB: n/2 and n/4 Fr per proof; points: k x L Fr
+void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* const* bufB, const Fr* points, int L,
+                            uint64_t n, Fr* const* last, hipStream_t s);
+// per proof j: nruns (<= 3) runs of `per` Fr from src[j].t[i] to dst[j] back to back, one launch
+void launch_copy_runs_group(int k, const Tables3* src, int nruns, int per, Fr* const* dst, hipStream_t s);
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
 // the last levels of an opening in one launch: how many of the `remaining` levels starting at a level
 // of `half` pairs it takes (0: none), and the launch (points[j] folds level j; q receives the levels'

@@ -14,6 +14,8 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <type_traits>
+#include <vector>
 #include <stdexcept>
 
 namespace spx {
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* 
 // bytes). Entry e: out_m[row] = val[e] * z[col[e]]; exactly one entry per (row, matrix), so products
 // are stored, never accumulated. No atomics, no counters.
 static constexpr uint32_t kSpmvPer = 4;  // entries per thread per chunk
-__global__ __launch_bounds__(kThreads) void k_spmv_sliced(SpmvSlicedView v, const Fr* __restrict__ z, Fr* o0, Fr* o1,
+DEV void k_spmv_sliced_body(SpmvSlicedView v, const Fr* __restrict__ z, Fr* o0, Fr* o1,
                                                           Fr* o2, uint64_t entries) {
     constexpr uint64_t kChunkE = kThreads * kSpmvPer;
     const uint64_t d = blockIdx.x & 7u, q = blockIdx.x >> 3, Q = gridDim.x >> 3;
@@ -271,6 +273,11 @@ __global__ __launch_bounds__(kThreads) void k_spmv_sliced(SpmvSlicedView v, cons
         }
     }
 }
+__global__ __launch_bounds__(kThreads) void k_spmv_sliced(SpmvSlicedView v, const Fr* __restrict__ z, Fr* o0, Fr* o1,
+                                                          Fr* o2, uint64_t entries) {
+    k_spmv_sliced_body(v, z, o0, o1, o2, entries);
+}
+
 
 // eval_on_x over the column stream (kernels.hpp: ColStreamView). eq(r_x, x) is never materialised:
 // it factors as lo[x & (2^klo - 1)] * hi[x >> klo] over the low and high variables (eq.rs:5-20 in
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_sliced(SpmvSlicedView v, cons
 // Two Montgomery products per entry at the product's measured issue rate (~4 cycles per instruction)
 // put the floor near 72 us at 2^20, well above the 19 us of its HBM bytes; loading the
 // row words a step ahead measured no gain.
-__global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFactors ef, Fr* __restrict__ out) {
+DEV void k_col_stream_body(ColStreamView cv, EqFactors ef, Fr* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const Fr* __restrict__ lo = ef.t[0];
     const Fr* __restrict__ hi3 = ef.t[1];
@@ -325,6 +332,10 @@ __global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFac
         if (info != kColNone) st_fr(out + (info & 0x3FFFFFFu), acc);
     }
 }
+__global__ __launch_bounds__(kThreads) void k_col_stream(ColStreamView cv, EqFactors ef, Fr* __restrict__ out) {
+    k_col_stream_body(cv, ef, out);
+}
+
 
 // long columns: one block per chunk of <= kChunk entries of one matrix; partial[chunk] = sum over the
 // chunk of val * eq(r_x, row) * r_m, the factor tables read from global memory (EqFactors)
@@ -399,7 +410,7 @@ __global__ void k_sparse_long_finish(const LongRow* __restrict__ rows, int nrows
 // variables computed directly in LDS (k / 2 + 1 dependent products deep, no per-variable barrier),
 // one product per output entry.
 static constexpr int kEqThreads = 1024;
-__global__ __launch_bounds__(kEqThreads) void k_eq_factors(const Fr* __restrict__ r, EqFactors ef,
+DEV void k_eq_factors_body(const Fr* __restrict__ r, EqFactors ef,
                                                            const Fr* __restrict__ scale) {
     __shared__ Fr A[64], B[128 * 3];
     const int f = blockIdx.x;
@@ -449,9 +460,14 @@ __global__ __launch_bounds__(kEqThreads) void k_eq_factors(const Fr* __restrict_
         }
     }
 }
+__global__ __launch_bounds__(kEqThreads) void k_eq_factors(const Fr* __restrict__ r, EqFactors ef,
+                                                           const Fr* __restrict__ scale) {
+    k_eq_factors_body(r, ef, scale);
+}
+
 
 // out[i] = lo[(i + base) & mask] * hi[(i + base) >> klo],  i < count
-__global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ lo, const Fr* __restrict__ hi, int klo,
+DEV void k_eq_expand_body(const Fr* __restrict__ lo, const Fr* __restrict__ hi, int klo,
                                                         uint64_t base, uint64_t count, Fr* __restrict__ out) {
     const uint64_t mask = (1ull << klo) - 1;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -461,6 +477,11 @@ __global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ l
         st_fr(out + i, t);
     }
 }
+__global__ __launch_bounds__(kThreads) void k_eq_expand(const Fr* __restrict__ lo, const Fr* __restrict__ hi, int klo,
+                                                        uint64_t base, uint64_t count, Fr* __restrict__ out) {
+    k_eq_expand_body(lo, hi, klo, base, count, out);
+}
+
 
 // ------------------------------------------------------------------ sumcheck #1 round
 // FOLD == false (round 1): X_t = in[2b + t];            e = E[b]
@@ -975,7 +996,7 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
 // ------------------------------------------------------------------ mKZG open level (open.rs:42-45)
 // q[b] = r[2b+1] - r[2b];  r'[b] = r[2b] + p * q[b]   ( = r[2b](1-p) + r[2b+1] p )
 // q may be null (fold only: the commitment-stubbed mode evaluates z without quotients)
-__global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+DEV void k_open_level_body(const Fr* __restrict__ rin, Fr* __restrict__ rout,
                                                          Fr* __restrict__ q, const Fr p, uint64_t half) {
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
@@ -987,6 +1008,11 @@ __global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ 
         st_fr(rout + b, t);
     }
 }
+__global__ __launch_bounds__(kThreads) void k_open_level(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+                                                         Fr* __restrict__ q, const Fr p, uint64_t half) {
+    k_open_level_body(rin, rout, q, p, half);
+}
+
 
 // NF consecutive levels of an opening in one launch: thread b takes the 2^NF entries
 // rin[2^NF b ..] and runs the NF folds in registers, writing level j's 2^(NF-1-j) quotients to
@@ -998,7 +1024,7 @@ struct FoldArgs {
     uint64_t qoff[NF];
 };
 template <int NF>
-__global__ __launch_bounds__(kThreads) void k_open_fold(const Fr* __restrict__ rin, Fr* __restrict__ rout, Fr* __restrict__ q,
+DEV void k_open_fold_body(const Fr* __restrict__ rin, Fr* __restrict__ rout, Fr* __restrict__ q,
                                                         FoldArgs<NF> a, uint64_t nout) {
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nout; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr v[1 << NF];
@@ -1019,6 +1045,12 @@ __global__ __launch_bounds__(kThreads) void k_open_fold(const Fr* __restrict__ r
         st_fr(rout + b, v[0]);
     }
 }
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold(const Fr* __restrict__ rin, Fr* __restrict__ rout, Fr* __restrict__ q,
+                                                        FoldArgs<NF> a, uint64_t nout) {
+    k_open_fold_body<NF>(rin, rout, q, a, nout);
+}
+
 
 // k_open_fold with every global access lane-contiguous (the wave-transposed form of the sumcheck
 // rounds above). A lane folds one group of 4 consecutive entries through two levels (2 + 1
@@ -1050,7 +1082,7 @@ DEV void wave_store_1(Fr* __restrict__ dst, const Fr& x, uint4* lds, int lane) {
     wave_rows_out<2>(reinterpret_cast<uint4*>(dst), lds, o, lane);
 }
 template <int NF>
-__global__ __launch_bounds__(kThreads) void k_open_fold_wave(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+DEV void k_open_fold_wave_body(const Fr* __restrict__ rin, Fr* __restrict__ rout,
                                                              Fr* __restrict__ q, FoldArgs<NF> a, uint64_t nout) {
     static_assert(NF == 2 || NF == 3, "2 or 3 levels");
     __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
@@ -1103,6 +1135,12 @@ __global__ __launch_bounds__(kThreads) void k_open_fold_wave(const Fr* __restric
         }
     }
 }
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold_wave(const Fr* __restrict__ rin, Fr* __restrict__ rout,
+                                                             Fr* __restrict__ q, FoldArgs<NF> a, uint64_t nout) {
+    k_open_fold_wave_body<NF>(rin, rout, q, a, nout);
+}
+
 
 // The last levels of an opening in ONE launch (one block, the table in LDS): level j folds
 // half = h0 >> j pairs, q_j = the level's quotients (q + qoff_j, contiguous), r' as k_open_level.
@@ -1112,7 +1150,7 @@ static constexpr int kTailMax = 512;  // largest first half of the tail (LDS: 2 
 struct TailPoints {
     Fr p[kTailMax <= 512 ? 10 : 20];
 };
-__global__ __launch_bounds__(kTailMax) void k_open_tail(const Fr* __restrict__ rin, Fr* __restrict__ q, uint32_t h0,
+DEV void k_open_tail_body(const Fr* __restrict__ rin, Fr* __restrict__ q, uint32_t h0,
                                                         int nlev, TailPoints pts, Fr* __restrict__ last) {
     __shared__ Fr buf[2 * kTailMax];
     for (uint32_t b = threadIdx.x; b < 2 * h0; b += blockDim.x) buf[b] = ld_fr(rin + b);
@@ -1137,6 +1175,100 @@ __global__ __launch_bounds__(kTailMax) void k_open_tail(const Fr* __restrict__ r
         half >>= 1;
     }
     if (threadIdx.x == 0) st_fr(last, buf[0]);
+}
+__global__ __launch_bounds__(kTailMax) void k_open_tail(const Fr* __restrict__ rin, Fr* __restrict__ q, uint32_t h0,
+                                                        int nlev, TailPoints pts, Fr* __restrict__ last) {
+    k_open_tail_body(rin, q, h0, nlev, pts, last);
+}
+
+
+// ------------------------------------------------------------------ lockstep groups: the other steps
+// The same kernels for the k proofs of a lockstep group in one launch: proof j's blocks at blockIdx.y
+// = j with its own job (pointers, points), everything else shared. The bodies see blockIdx.x and
+// gridDim.x of their own proof, as in the per-proof launch (k_spmv_sliced's XCD eighths included: the
+// per-proof grid is a multiple of 8, so the linear workgroup id keeps blockIdx.x mod 8).
+template <class J>
+struct GroupOf {
+    J j[kGroupMax];
+};
+struct SpmvJob {
+    const Fr* z;
+    Fr* o[3];
+};
+struct EqfJob {
+    const Fr* r;
+    EqFactors ef;
+    const Fr* scale;
+};
+struct EqxJob {
+    const Fr* lo;
+    const Fr* hi;
+    Fr* out;
+};
+struct ColJob {
+    EqFactors ef;
+    Fr* out;
+};
+template <int NF>
+struct FoldJob {
+    const Fr* rin;
+    Fr* rout;
+    FoldArgs<NF> a;
+};
+struct LevelJob {
+    const Fr* rin;
+    Fr* rout;
+    Fr p;
+};
+struct TailJob {
+    const Fr* rin;
+    Fr* last;
+    TailPoints pts;
+};
+struct CopyJob {  // up to 3 runs of `per` Fr -> dst, back to back
+    const Fr* src[3];
+    Fr* dst;
+};
+__global__ __launch_bounds__(kThreads) void k_spmv_sliced_group(SpmvSlicedView v, GroupOf<SpmvJob> g, uint64_t entries) {
+    const SpmvJob& j = g.j[blockIdx.y];
+    k_spmv_sliced_body(v, j.z, j.o[0], j.o[1], j.o[2], entries);
+}
+__global__ __launch_bounds__(kEqThreads) void k_eq_factors_group(GroupOf<EqfJob> g) {
+    const EqfJob& j = g.j[blockIdx.y];
+    k_eq_factors_body(j.r, j.ef, j.scale);
+}
+__global__ __launch_bounds__(kThreads) void k_eq_expand_group(GroupOf<EqxJob> g, int klo, uint64_t base, uint64_t count) {
+    const EqxJob& j = g.j[blockIdx.y];
+    k_eq_expand_body(j.lo, j.hi, klo, base, count, j.out);
+}
+__global__ __launch_bounds__(kThreads) void k_col_stream_group(ColStreamView cv, GroupOf<ColJob> g) {
+    const ColJob& j = g.j[blockIdx.y];
+    k_col_stream_body(cv, j.ef, j.out);
+}
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold_group(GroupOf<FoldJob<NF>> g, uint64_t nout) {
+    const FoldJob<NF>& j = g.j[blockIdx.y];
+    k_open_fold_body<NF>(j.rin, j.rout, nullptr, j.a, nout);
+}
+template <int NF>
+__global__ __launch_bounds__(kThreads) void k_open_fold_wave_group(GroupOf<FoldJob<NF>> g, uint64_t nout) {
+    const FoldJob<NF>& j = g.j[blockIdx.y];
+    k_open_fold_wave_body<NF>(j.rin, j.rout, nullptr, j.a, nout);
+}
+__global__ __launch_bounds__(kThreads) void k_open_level_group(GroupOf<LevelJob> g, uint64_t half) {
+    const LevelJob& j = g.j[blockIdx.y];
+    k_open_level_body(j.rin, j.rout, nullptr, j.p, half);
+}
+__global__ __launch_bounds__(kTailMax) void k_open_tail_group(GroupOf<TailJob> g, uint32_t h0, int nlev) {
+    const TailJob& j = g.j[blockIdx.y];
+    k_open_tail_body(j.rin, nullptr, h0, nlev, j.pts, j.last);
+}
+// proof blockIdx.x: n runs of `per` Fr (src[i][0 .. per)) -> dst[per i ..] (host-mapped pinned memory:
+// a group's small device-to-host results in one launch instead of a copy per run)
+__global__ void k_copy_runs_group(GroupOf<CopyJob> g, int n, int per) {
+    const CopyJob& j = g.j[blockIdx.x];
+    const int t = threadIdx.x;
+    if (t < n * per) st_fr(j.dst + t, ld_fr(j.src[t / per] + t % per));
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1412,6 +1544,122 @@ void launch_sc2_round_group(int k, bool fold, const Sc2Job* jobs, uint64_t half,
     kp_end(32.0 * (double)k * (double)half * (fold ? 12.0 : 4.0), s);
     if (g > kFuseMaxBlocks)
         hipLaunchKernelGGL(k_reduce_partials_group<Sc2Group>, dim3(k), dim3(kThreads), 0, s, G, g);
+}
+
+// ---- the other steps of a lockstep group (prove_group), one launch per step for the k proofs
+template <class J>
+static GroupOf<J> group_check(int k) {
+    if (k < 1 || k > kGroupMax) throw std::invalid_argument("lockstep group size out of range");
+    return GroupOf<J>{};
+}
+void launch_spmv_sliced_group(int k, const SpmvSlicedView& v, const Fr* const* z, const Tables3* out, uint64_t entries,
+                              hipStream_t s) {
+    GroupOf<SpmvJob> g = group_check<SpmvJob>(k);
+    for (int i = 0; i < k; ++i) g.j[i] = SpmvJob{z[i], {out[i].t[0], out[i].t[1], out[i].t[2]}};
+    const uint64_t per_xcd = (entries / 8 + kThreads * kSpmvPer - 1) / (kThreads * kSpmvPer);
+    const uint32_t Q = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (per_xcd + 1) / 2));
+    hipLaunchKernelGGL(k_spmv_sliced_group, dim3(8 * Q, k), dim3(kThreads), 0, s, v, g, entries);
+}
+void launch_eq_table_group(int k, const Fr* const* r_dev, int nvar, uint64_t base, uint64_t count, Fr* const* out,
+                           Fr* const* lo, Fr* const* hi, hipStream_t s) {
+    const int klo = (nvar + 1) / 2, khi = nvar - klo;
+    if (nvar < 0 || klo > 13) throw std::invalid_argument("launch_eq_table_group: more than 26 variables");
+    GroupOf<EqfJob> gf = group_check<EqfJob>(k);
+    GroupOf<EqxJob> gx = group_check<EqxJob>(k);
+    for (int i = 0; i < k; ++i) {
+        EqFactors ef{};
+        ef.nf = 2;
+        ef.k[0] = klo;
+        ef.k[1] = khi;
+        ef.t[0] = lo[i];
+        ef.t[1] = hi[i];
+        gf.j[i] = EqfJob{r_dev[i], ef, nullptr};
+        gx.j[i] = EqxJob{lo[i], hi[i], out[i]};
+    }
+    hipLaunchKernelGGL(k_eq_factors_group, dim3(2, k), dim3(kEqThreads), 0, s, gf);
+    kp_begin(KP_EQ, s);
+    hipLaunchKernelGGL(k_eq_expand_group, dim3(grid_for(count, 8192), k), dim3(kThreads), 0, s, gx, klo, base, count);
+    kp_end(32.0 * (double)count * k, s);
+}
+void launch_col_stream_group(int k, const ColStreamView& cv, const Fr* const* r_x, int L, const Fr* const* scale,
+                             Fr* const* out, Fr* const* eq_scratch, hipStream_t s) {
+    GroupOf<EqfJob> gf = group_check<EqfJob>(k);
+    GroupOf<ColJob> gc = group_check<ColJob>(k);
+    int nf = 0;
+    for (int i = 0; i < k; ++i) {
+        const EqFactors ef = eq_factors_for(L, eq_scratch[i]);
+        nf = ef.nf;
+        gf.j[i] = EqfJob{r_x[i], ef, scale[i]};
+        gc.j[i] = ColJob{ef, out[i]};
+    }
+    hipLaunchKernelGGL(k_eq_factors_group, dim3(nf, k), dim3(kEqThreads), 0, s, gf);
+    if (cv.nslices) {
+        const uint32_t nwin = (cv.nslices + kColWindow - 1) / kColWindow;
+        hipLaunchKernelGGL(k_col_stream_group, dim3(nwin, k), dim3(kThreads), 0, s, cv, gc);
+    }
+}
+void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* const* bufB, const Fr* points, int L,
+                            uint64_t n, Fr* const* last, hipStream_t s) {
+    group_check<LevelJob>(k);
+    std::vector<const Fr*> rin(z, z + k);
+    kp_begin(KP_OPEN, s);
+    bool tail = false;
+    int nb = 0;
+    for (int i = 0; i < L;) {
+        Fr* const* rout = (nb++ & 1) ? bufB : bufA;
+        const uint64_t half = n >> (i + 1);
+        if (open_tail_levels(half, L - i) == L - i) {  // the remaining levels, straight into `last`
+            GroupOf<TailJob> g{};
+            for (int j = 0; j < k; ++j) {
+                g.j[j].rin = rin[j];
+                g.j[j].last = last[j];
+                for (int q = i; q < L; ++q) g.j[j].pts.p[q - i] = points[(size_t)j * L + q];
+            }
+            hipLaunchKernelGGL(k_open_tail_group, dim3(1, k), dim3(kTailMax), 0, s, g, (uint32_t)half, L - i);
+            tail = true;
+            break;
+        }
+        const int nf = L - i >= 3 && (half >> 2) >= 1 ? 3 : (L - i >= 2 && (half >> 1) >= 1 ? 2 : 1);
+        const uint64_t nout = n >> (i + nf);
+        if (nf == 3 || nf == 2) {
+            auto run = [&](auto tag) {
+                constexpr int NF = decltype(tag)::value;
+                GroupOf<FoldJob<NF>> g{};
+                for (int j = 0; j < k; ++j) {
+                    g.j[j].rin = rin[j];
+                    g.j[j].rout = rout[j];
+                    for (int q = 0; q < NF; ++q) g.j[j].a.p[q] = points[(size_t)j * L + i + q], g.j[j].a.qoff[q] = ~0ull;
+                }
+                if (nout >= kWaveMinHalf)
+                    hipLaunchKernelGGL(k_open_fold_wave_group<NF>, dim3(grid_for(nout, 8192), k), dim3(kThreads), 0, s, g,
+                                       nout);
+                else
+                    hipLaunchKernelGGL(k_open_fold_group<NF>, dim3(grid_for(nout, 8192), k), dim3(kThreads), 0, s, g, nout);
+            };
+            if (nf == 3)
+                run(std::integral_constant<int, 3>{});
+            else
+                run(std::integral_constant<int, 2>{});
+        } else {
+            GroupOf<LevelJob> g{};
+            for (int j = 0; j < k; ++j) g.j[j] = LevelJob{rin[j], rout[j], points[(size_t)j * L + i]};
+            hipLaunchKernelGGL(k_open_level_group, dim3(grid_for(half, 8192), k), dim3(kThreads), 0, s, g, half);
+        }
+        for (int j = 0; j < k; ++j) rin[j] = rout[j];
+        i += nf;
+    }
+    kp_end(32.0 * 2.0 * (double)n * k, s);  // reads ~2n over the levels, writes ~n
+    if (!tail) {  // the chain ended on a fold: its one-entry table to `last`
+        GroupOf<CopyJob> g{};
+        for (int j = 0; j < k; ++j) g.j[j] = CopyJob{{rin[j], nullptr, nullptr}, last[j]};
+        hipLaunchKernelGGL(k_copy_runs_group, dim3(k), dim3(64), 0, s, g, 1, 1);
+    }
+}
+void launch_copy_runs_group(int k, const Tables3* src, int nruns, int per, Fr* const* dst, hipStream_t s) {
+    GroupOf<CopyJob> g = group_check<CopyJob>(k);
+    if (nruns < 1 || nruns > 3 || per < 1 || nruns * per > 64) throw std::invalid_argument("launch_copy_runs_group");
+    for (int j = 0; j < k; ++j) g.j[j] = CopyJob{{src[j].t[0], src[j].t[1], src[j].t[2]}, dst[j]};
+    hipLaunchKernelGGL(k_copy_runs_group, dim3(k), dim3(64), 0, s, g, nruns, per);
 }
 
 int open_tail_levels(uint64_t half, int remaining) {

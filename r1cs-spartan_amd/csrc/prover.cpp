@@ -1601,15 +1601,20 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
     // per-proof scratch, prove()'s layout at G = 1
     const uint64_t n2 = std::max<uint64_t>(nl / 2, 1), n4 = std::max<uint64_t>(nl / 4, 1);
     const uint64_t npart = std::max<uint64_t>(kRoundPartials, std::max(I.rows.nchunks, I.cols.longc.nchunks));
+    // (plus the opening folds' two buffers per proof: the group's fold chains run side by side)
     const uint64_t need = 3 * nl + 3 * n2 + 3 * n4 + n2 + n4 + std::max<uint64_t>(nl / 8, 1) + nl + n2 + n4 + n2 + n4 +
-                          npart + 8192 * 2 + kEqScratch + 64 + 8 * L;
-    C.scratch.ensure(32 * need * (uint64_t)k);
+                          npart + 8192 * 2 + kEqScratch + 64 + n2 + n4;
+    // the group's challenges: proof j's tau, r_x, r_abc at chg + 8 L j (one host-to-device copy each time)
+    C.scratch.ensure(32 * (need + 8 * (uint64_t)L) * (uint64_t)k);
+    Fr* chg = C.scratch.as<Fr>() + need * k;
     static_assert(kGroupMax * 8192 <= (64 << 10), "per-proof pinned regions");
-    if (32 * (L + 3) > 4096 || 32 * (L + 1) > 2048) invalid("log_n too large for a lockstep group");
+    if (32 * (L + 3) > 4096 || 32 * 8 * L * kGroupMax > (64 << 10)) invalid("log_n too large for a lockstep group");
     uint8_t* hp0 = C.pin_at(Ctx::kPinHp, kGroupMax * 8192, 64 << 10);
     uint8_t* ho0 = C.pin_at(Ctx::kPinOpen, kGroupMax * 2048, 56 << 10);
+    uint8_t* stage = C.pin_at(Ctx::kPinStage, (size_t)32 * 8 * L * k, 64 << 10);
     struct P {
         Fr *Az, *Bz, *Cz, *F1[3], *F2[3], *E1, *Ea, *Eb, *M0, *M1, *M2, *Z1, *Z2, *partial, *eqlo, *eqhi, *eqf, *chdev;
+        Fr *oA, *oB;
         uint8_t *hp, *ho;
         Fr* res_dev;
         const Fr* z;
@@ -1641,7 +1646,8 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         p.Z1 = take(n2), p.Z2 = take(n4);
         p.partial = take(npart);
         p.eqlo = take(8192), p.eqhi = take(8192), p.eqf = take(kEqScratch);
-        p.chdev = take(8 * L);
+        p.oA = take(n2), p.oB = take(n4);
+        p.chdev = chg + (uint64_t)8 * L * j;
         p.hp = hp0 + 8192 * j;
         p.ho = ho0 + 2048 * j;
         p.res_dev = C.pin_dev<Fr>(p.hp);
@@ -1650,15 +1656,24 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         p.T = Transcript(os[j].mode == 1, os[j].seed, nullptr);
         ps.push_back(std::move(p));
     }
+    // per-proof pointer arrays for the group launchers
+    auto each = [&](auto f) {
+        using T = decltype(f(ps[0]));
+        std::vector<T> v;
+        for (auto& p : ps) v.push_back(f(p));
+        return v;
+    };
     // ---- SpMV Az, Bz, Cz of every proof (challenge-independent)
-    for (auto& p : ps) {
+    if (I.rows_sliced.on) {
         kp_begin(KP_SPMV, C.stream);
-        if (I.rows_sliced.on)
-            launch_spmv_sliced(I.rows_sliced.view(), p.z, p.Az, p.Bz, p.Cz, I.rows_sliced.entries, C.stream);
-        else
+        const auto zs = each([](P& p) -> const Fr* { return p.z; });
+        const auto outs = each([](P& p) { return Tables3{{p.Az, p.Bz, p.Cz}}; });
+        launch_spmv_sliced_group(k, I.rows_sliced.view(), zs.data(), outs.data(), I.rows_sliced.entries, C.stream);
+        kp_end(I.rows_bytes * k, C.stream);
+    } else {
+        for (auto& p : ps)
             launch_sparse3(0, I.rows.view(), p.z, p.Az, p.Bz, p.Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(),
                            I.rows.nchunks, I.rows.lrows.as<LongRow>(), I.rows.nlrows, p.partial, C.stream);
-        kp_end(I.rows_bytes, C.stream);
     }
     // ---- transcripts: A, B, C (cached or absorbed), v; round 1 with the stubbed commitment
     for (int j = 0; j < k; ++j) {
@@ -1682,39 +1697,17 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         p.proof.raw(b, 48);
         p.T.feed(p.proof.b.data(), p.proof.b.size());
     }
-    // stubbed openings of every proof's z (open_stub's launches; the chains share the fold buffers, in
-    // stream order) and one wait
-    Fr* obuf[2] = {C.buf<Fr>(Ctx::kSlotOpenA, 32 * std::max<uint64_t>(nl / 2, 1)),
-                   C.buf<Fr>(Ctx::kSlotOpenB, 32 * std::max<uint64_t>(nl / 4, 1))};
+    // stubbed openings: every proof's z(point) by open_stub's fold chain, one launch per step for the
+    // group, the values written straight into pinned memory; one wait
     auto open_all = [&](const std::vector<std::vector<HFr>>& pts) {
-        for (int j = 0; j < k; ++j) {
-            const std::vector<HFr>& point = pts[j];
-            const Fr* rin = ps[j].z;
-            int nb = 0;
-            for (int i = 0; i < L;) {
-                Fr* rout = obuf[nb++ & 1];
-                const uint64_t half = nl >> (i + 1);
-                if (open_tail_levels(half, L - i) == L - i) {
-                    std::vector<Fr> tp(L - i);
-                    for (int q = i; q < L; ++q) tp[q - i] = dev_fr(point[q]);
-                    launch_open_tail(rin, nullptr, half, L - i, tp.data(), rout, C.stream);
-                    rin = rout;
-                    break;
-                }
-                const int nf = L - i >= 3 && (half >> 2) >= 1 ? 3 : (L - i >= 2 && (half >> 1) >= 1 ? 2 : 1);
-                if (nf >= 2) {
-                    Fr fp[3];
-                    uint64_t qoffs[3] = {~0ull, ~0ull, ~0ull};
-                    for (int q = 0; q < nf; ++q) fp[q] = dev_fr(point[i + q]);
-                    launch_open_fold(rin, rout, nullptr, nf, fp, qoffs, nl >> (i + nf), C.stream);
-                } else {
-                    launch_open_level(rin, rout, nullptr, dev_fr(point[i]), half, C.stream);
-                }
-                rin = rout;
-                i += nf;
-            }
-            SPX_HIP(hipMemcpyAsync(ps[j].ho, rin, 32, hipMemcpyDeviceToHost, C.stream));
-        }
+        std::vector<Fr> flat((size_t)k * L);
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i < L; ++i) flat[(size_t)j * L + i] = dev_fr(pts[j][i]);
+        const auto zs = each([](P& p) -> const Fr* { return p.z; });
+        const auto as = each([](P& p) { return p.oA; });
+        const auto bs = each([](P& p) { return p.oB; });
+        const auto last = each([&](P& p) { return C.pin_dev<Fr>(p.ho); });
+        launch_open_eval_group(k, zs.data(), as.data(), bs.data(), flat.data(), L, nl, last.data(), C.stream);
         C.sync();
         const std::vector<Affine<HFq2>> none(L, Affine<HFq2>{HFq2::zero(), HFq2::zero(), true});
         for (int j = 0; j < k; ++j) {
@@ -1732,15 +1725,23 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         }
         open_all(pts);
     }
-    // ---- round 3: tau, eq table; sumcheck 1 setup
-    for (auto& p : ps) {
+    // ---- round 3: tau (one copy for the group), eq tables (one launch pair); sumcheck 1 setup
+    for (int j = 0; j < k; ++j) {
+        P& p = ps[j];
         p.tau.resize(L);
         for (int i = 0; i < L; ++i) p.tau[i] = p.T.rand_fr();
-        memcpy(p.hp, p.tau.data(), 32 * L);
-        SPX_HIP(hipMemcpyAsync(p.chdev, p.hp, 32 * L, hipMemcpyHostToDevice, C.stream));
-        if (L >= 2)
-            launch_eq_table(p.chdev + 1, L - 1, 0, nl / 2, p.E1, p.eqlo, p.eqhi, C.stream);
-        else {
+        memcpy(stage + (size_t)32 * 8 * L * j, p.tau.data(), 32 * L);
+    }
+    SPX_HIP(hipMemcpyAsync(chg, stage, (size_t)32 * 8 * L * k, hipMemcpyHostToDevice, C.stream));
+    if (L >= 2) {
+        const auto rs = each([](P& p) -> const Fr* { return p.chdev + 1; });
+        const auto outs = each([](P& p) { return p.E1; });
+        const auto lo = each([](P& p) { return p.eqlo; });
+        const auto hi = each([](P& p) { return p.eqhi; });
+        launch_eq_table_group(k, rs.data(), L - 1, 0, nl / 2, outs.data(), lo.data(), hi.data(), C.stream);
+    }
+    for (auto& p : ps) {
+        if (L < 2) {
             const HFr one = HFr::one();
             memcpy(p.hp + 4096, &one, 32);
             SPX_HIP(hipMemcpyAsync(p.E1, p.hp + 4096, 32, hipMemcpyHostToDevice, C.stream));
@@ -1811,8 +1812,11 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         }
     }
     // the tables hold 2 entries each: bind r_L on the host (prove()'s G = 1 case)
-    for (auto& p : ps)
-        for (int m = 0; m < 3; ++m) SPX_HIP(hipMemcpyAsync(p.hp + 64 * m, p.cur.t[m], 64, hipMemcpyDeviceToHost, C.stream));
+    {
+        const auto src = each([](P& p) { return p.cur; });
+        const auto dst = each([&](P& p) { return C.pin_dev<Fr>(p.hp); });
+        launch_copy_runs_group(k, src.data(), 3, 2, dst.data(), C.stream);
+    }
     C.sync();
     for (auto& p : ps) {
         const HFr r = p.r_x.back();
@@ -1826,14 +1830,10 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         for (int m = 0; m < 3; ++m) p.proof.fr(v[m]);
         p.T.feed(p.proof.b.data() + m0, p.proof.b.size() - m0);
         HFr rabc[3] = {p.T.rand_fr(), p.T.rand_fr(), p.T.rand_fr()};
-        // ---- round 5: M_rx (the previous wait covers the staging region's earlier copies)
-        Fr* rxdev = p.chdev + 2 * L;
-        memcpy(p.hp + 256, p.r_x.data(), 32 * L);
-        memcpy(p.hp + 256 + 32 * L, rabc, 96);
-        SPX_HIP(hipMemcpyAsync(rxdev, p.hp + 256, 32 * (L + 3), hipMemcpyHostToDevice, C.stream));
-        kp_begin(KP_MTV, C.stream);
-        I.cols.launch(rxdev, L, rxdev + L, p.M0, p.eqf, p.partial, C.stream);
-        kp_end(I.cols_bytes, C.stream);
+        // ---- round 5's challenges, staged for one copy (the waits above cover the stage's earlier copy)
+        uint8_t* st = stage + (size_t)32 * (8 * L * (&p - ps.data()) + 2 * L);
+        memcpy(st, p.r_x.data(), 32 * L);
+        memcpy(st + 32 * L, rabc, 96);
         m0 = p.proof.b.size();
         p.proof.u64(2);
         p.proof.u64((uint64_t)L);
@@ -1843,6 +1843,19 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         p.Mc = p.M0;
         p.Zc = p.z;
     }
+    // ---- round 5: M_rx = sum_m r_m M(r_x, .) of every proof
+    SPX_HIP(hipMemcpyAsync(chg, stage, (size_t)32 * 8 * L * k, hipMemcpyHostToDevice, C.stream));
+    kp_begin(KP_MTV, C.stream);
+    if (I.cols.longc.nchunks == 0) {
+        const auto rx = each([&](P& p) -> const Fr* { return p.chdev + 2 * L; });
+        const auto sc = each([&](P& p) -> const Fr* { return p.chdev + 3 * L; });
+        const auto outs = each([](P& p) { return p.M0; });
+        const auto eqs = each([](P& p) { return p.eqf; });
+        launch_col_stream_group(k, I.cols.view(), rx.data(), L, sc.data(), outs.data(), eqs.data(), C.stream);
+    } else {
+        for (auto& p : ps) I.cols.launch(p.chdev + 2 * L, L, p.chdev + 3 * L, p.M0, p.eqf, p.partial, C.stream);
+    }
+    kp_end(I.cols_bytes * k, C.stream);
     // ---- sumcheck 2
     std::vector<Sc2Job> j2(k);
     for (int i = 1; i <= L; ++i) {
@@ -1860,7 +1873,6 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
             jb.ticket = C.ticket + j;
             jb.result3 = p.res_dev;
         }
-        // (round 5's copies out of hp + 256 are ordered before this round's results land in hp)
         launch_sc2_round_group(k, fold, j2.data(), half, !fold || check_derived, C.stream);
         C.sync();
         for (int j = 0; j < k; ++j) {

@@ -409,10 +409,12 @@ def largest_rate(d):
 # 783-794 M). 8 / 16 / 32 hardware queues instead of 4: 542-666 M index-cached (r05w_c2_hwq.jsonl).
 # (Round 4, spinning: 32 in flight on 4 queues had halved the index-cached rate against 16.)
 # Lockstep groups (spx_ctx_set_group, round 5): each context proves C2_GROUP proofs at a time, every
-# sumcheck round of the group one launch and one wait. One-at-a-time C2 proofs left the GPU idle 65%
-# of the time behind the 4 hardware queues (r05zg_c2_busy.txt); index-cached 790 M -> 1,166 M with 8
-# contexts x 4, 1,335 M with 8 x 8, 1,454 - 1,461 M with 16 x 8 (more queues: lower;
-# profiles/r05/r05zh_c2group.jsonl, r05zi_c2group.jsonl). C2_INFLIGHT counts proofs in flight.
+# step of the group (sumcheck round, SpMV, eq table, eval_on_x, opening fold) one launch and every
+# round one wait. One-at-a-time C2 proofs left the GPU idle 65% of the time behind the 4 hardware
+# queues (r05zg_c2_busy.txt); index-cached 790 M -> 1,454 - 1,461 M with 16 contexts x 8 and the
+# sumcheck rounds grouped (more queues: lower; profiles/r05/r05zh_c2group.jsonl, r05zi_c2group.jsonl),
+# 2,114 - 2,190 M with every step grouped (r05zl_c2group.jsonl; 64 / 128 / 192 / 256 in flight: 1,987 /
+# 2,142 - 2,165 / 2,114 - 2,122 / 2,137 - 2,190 M). C2_INFLIGHT counts proofs in flight.
 C2_INFLIGHT = 128
 C2_GROUP = 8
 C2_SYNC_POLL_US = 20
@@ -1148,6 +1150,19 @@ def c2_line(spx, L, args, B):
     stats = kernel_stats(spx, L, ctxs[0], steps)
     spx._check(L.spx_kernel_stats_enable(ctxs[0].h, 0))
     assert p1 == proofs[0]
+    # one lockstep group alone (the launches the pipeline runs: each step of C2_GROUP proofs in one launch)
+    spx._check(L.spx_kernel_stats_enable(ctxs[0].h, 1))
+    for _ in range(steps):
+        pg = spx.MLArgumentForR1CS.prove_many([ctxs[0]], pk, wits[:C2_GROUP], None, mode=args.mode, seed=7, cached=True,
+                                              commitment_stub=True)
+    gstats = kernel_stats(spx, L, ctxs[0], steps * C2_GROUP)
+    spx._check(L.spx_kernel_stats_enable(ctxs[0].h, 0))
+    assert pg == proofs[:C2_GROUP]
+    rgroup = roofline_hbm(gstats, None)
+    if rgroup:
+        rgroup["note"] = ("one lockstep group of %d proofs alone: algorithmic bytes of the kernel's largest group "
+                          "launch (all %d proofs) / its HIP-event duration; traffic: no PMC pass of the group "
+                          "kernels" % (C2_GROUP, C2_GROUP))
     # the same pipeline with the matrices absorbed once at index time (bit-identical proofs): the GPU
     # side's capacity, which the per-proof host hashing hides in `value`
     t0 = time.perf_counter()
@@ -1165,6 +1180,7 @@ def c2_line(spx, L, args, B):
         "value_index_cached_transcript": round(steps * P * n / elc, 1),
         "kernels_ms_per_proof": {k: round(v["ms"], 4) for k, v in stats.items()},
         "roofline": roofline_hbm(stats, PMC_FILE_C2),
+        "roofline_group": rgroup,
         "hashing_cores_busy": round((hs1[0] - hs0[0]) / el, 2),
     }
     if not args.no_cpu:

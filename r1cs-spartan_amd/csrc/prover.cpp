@@ -1573,6 +1573,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
 // steps queue the k proofs' launches back to back before one wait. Every value is computed by the same
 // kernels and host formulas as prove(), so each proof's bytes are its own prove()'s.
 std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* Ws, int k, const ProveOpts* os) {
+    static_assert(kGroupMax <= 16, "one sumcheck ticket per proof of a group: Ctx::ticket holds 16 counters");
     if (k < 1 || k > kGroupMax) invalid("lockstep group size must be 1.." + std::to_string(kGroupMax));
     CtxClaim claim;
     claim.take(C);

@@ -73,3 +73,17 @@ def test_group_size_checked(spx, ctx):
         with pytest.raises(spx.InvalidArgument):
             c.set_group(bad)
     c.set_group(1)
+
+
+@pytest.mark.gpu
+def test_group_with_device_checked_identities(spx, ctx, monkeypatch):
+    """SPX_CHECK_DERIVED=1: every round also computes the derived value on the device and checks it, so
+    every round of a group takes its G(1) / P(1) form: the large rounds' NEED1 group kernels and the small
+    rounds' per-proof launches inside a group (launch_sc1_round_group's fallback). Same bytes."""
+    log_n, log_v = 16, 3
+    syn, pk, wits = _instance(spx, ctx, log_n, log_v, 5)
+    want = [spx.MLArgumentForR1CS.prove_witness(pk, w, None, seed=5, commitment_stub=True) for w in wits]
+    monkeypatch.setenv("SPX_CHECK_DERIVED", "1")
+    c = spx.Context(0)
+    c.set_group(4)
+    assert spx.MLArgumentForR1CS.prove_many([c], pk, wits, None, seed=5, commitment_stub=True) == want

@@ -71,6 +71,9 @@ struct Tables3 {
 // proofs of one index, proof j's blocks at blockIdx.y = j, each with its own tables, challenge,
 // partials, ticket and result (the per-proof launches' arguments, passed by value)
 static constexpr int kGroupMax = 8;
+// the last rounds of each sumcheck a lockstep group runs on the host (prove_group): <= 5 (the tables
+// then fit each proof's 8 KiB pinned region)
+static constexpr int kGroupHostTail = 5;
 struct Sc1Job {
     Tables3 in, out;
     const Fr* Ein;
@@ -233,7 +236,8 @@ void launch_col_stream_group(int k, const ColStreamView& cv, const Fr* const* r_
 // (host-mapped pinned memory allowed); bufA / bufB: n/2 and n/4 Fr per proof; points: k x L Fr
 void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* const* bufB, const Fr* points, int L,
                             uint64_t n, Fr* const* last, hipStream_t s);
-// per proof j: nruns (<= 3) runs of `per` Fr from src[j].t[i] to dst[j] back to back, one launch
+// per proof j: nruns (<= 3) runs of `per` Fr (nruns x per <= 4096) from src[j].t[i] to dst[j] back to back,
+// one launch
 void launch_copy_runs_group(int k, const Tables3* src, int nruns, int per, Fr* const* dst, hipStream_t s);
 void launch_open_level(const Fr* rin, Fr* rout, Fr* q, const Fr& point, uint64_t half, hipStream_t s);
 // the last levels of an opening in one launch: how many of the `remaining` levels starting at a level

@@ -1267,8 +1267,7 @@ __global__ __launch_bounds__(kTailMax) void k_open_tail_group(GroupOf<TailJob> g
 // a group's small device-to-host results in one launch instead of a copy per run)
 __global__ void k_copy_runs_group(GroupOf<CopyJob> g, int n, int per) {
     const CopyJob& j = g.j[blockIdx.x];
-    const int t = threadIdx.x;
-    if (t < n * per) st_fr(j.dst + t, ld_fr(j.src[t / per] + t % per));
+    for (int t = threadIdx.x; t < n * per; t += blockDim.x) st_fr(j.dst + t, ld_fr(j.src[t / per] + t % per));
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1657,9 +1656,9 @@ void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* cons
 }
 void launch_copy_runs_group(int k, const Tables3* src, int nruns, int per, Fr* const* dst, hipStream_t s) {
     GroupOf<CopyJob> g = group_check<CopyJob>(k);
-    if (nruns < 1 || nruns > 3 || per < 1 || nruns * per > 64) throw std::invalid_argument("launch_copy_runs_group");
+    if (nruns < 1 || nruns > 3 || per < 1 || nruns * per > 4096) throw std::invalid_argument("launch_copy_runs_group");
     for (int j = 0; j < k; ++j) g.j[j] = CopyJob{{src[j].t[0], src[j].t[1], src[j].t[2]}, dst[j]};
-    hipLaunchKernelGGL(k_copy_runs_group, dim3(k), dim3(64), 0, s, g, nruns, per);
+    hipLaunchKernelGGL(k_copy_runs_group, dim3(k), dim3(256), 0, s, g, nruns, per);
 }
 
 int open_tail_levels(uint64_t half, int remaining) {

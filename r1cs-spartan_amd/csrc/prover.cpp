@@ -1757,10 +1757,17 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         p.cur = Tables3{{p.Az, p.Bz, p.Cz}};
         p.Ecur = p.E1;
     }
+    // The last ht rounds of each sumcheck run on the host (the tables are then <= 2^(ht+1) entries: a few
+    // microseconds of host arithmetic per round, against a ~30 us launch that holds one of the 4 hardware
+    // queues), with prove()'s formulas for the gathered tables of a sharded proof: the same field values.
+    // (2,216 - 2,221 M index-cached against 2,138 - 2,155 M with every round on the device, 3 or 4 rounds
+    // between: profiles/r05/r05zs_hosttail.jsonl)
+    static_assert(kGroupHostTail >= 0 && kGroupHostTail <= 5, "3 x 2^(ht+1) Fr fit each proof's 8 KiB pinned region");
+    const int ht = std::min(kGroupHostTail, L - 1);
     // ---- sumcheck 1: one launch and one wait per round for the group
     std::vector<Sc1Job> j1(k);
     std::vector<char> derive(k);
-    for (int i = 1; i <= L; ++i) {
+    for (int i = 1; i <= L - ht; ++i) {
         const uint64_t half = nl >> i;
         const bool fold = i >= 2;
         bool need1 = check_derived;
@@ -1812,20 +1819,56 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
             }
         }
     }
-    // the tables hold 2 entries each: bind r_L on the host (prove()'s G = 1 case)
+    // the tables hold tn = 2^(ht+1) entries each: bind r_{L-ht} on the host, then the host rounds
+    const uint32_t tn = 2u << ht;
     {
         const auto src = each([](P& p) { return p.cur; });
         const auto dst = each([&](P& p) { return C.pin_dev<Fr>(p.hp); });
-        launch_copy_runs_group(k, src.data(), 3, 2, dst.data(), C.stream);
+        launch_copy_runs_group(k, src.data(), 3, (int)tn, dst.data(), C.stream);
     }
     C.sync();
     for (auto& p : ps) {
-        const HFr r = p.r_x.back();
-        HFr v[3];
-        for (int m = 0; m < 3; ++m) {
-            const HFr a0 = ld_hfr(p.hp + 64 * m), a1 = ld_hfr(p.hp + 64 * m + 32);
-            v[m] = a0 + r * (a1 - a0);
+        std::vector<HFr> tabs[3];
+        {
+            const HFr r = p.r_x.back();
+            for (int m = 0; m < 3; ++m)
+                for (uint32_t b = 0; b < tn / 2; ++b) {
+                    const HFr a0 = ld_hfr(p.hp + 32 * (m * tn + 2 * b)), a1 = ld_hfr(p.hp + 32 * (m * tn + 2 * b + 1));
+                    tabs[m].push_back(a0 + r * (a1 - a0));
+                }
         }
+        for (int i = L - ht + 1; i <= L; ++i) {  // prove()'s rounds on gathered tables
+            const size_t half = tabs[0].size() / 2;
+            const int c = i - 1;
+            HFr gs[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
+            for (size_t b = 0; b < half; ++b) {
+                HFr e = HFr::one();  // eq(tau_{c+1..L-1}, b)
+                for (int jj = c + 1; jj < L; ++jj) e *= ((b >> (jj - c - 1)) & 1) ? p.tau[jj] : HFr::one() - p.tau[jj];
+                HFr x0[3], x1[3], y[3];
+                for (int m = 0; m < 3; ++m) {
+                    x0[m] = tabs[m][2 * b];
+                    x1[m] = tabs[m][2 * b + 1];
+                    y[m] = x1[m] + x1[m] - x0[m];
+                }
+                gs[0] += (x0[0] * x0[1] - x0[2]) * e;
+                gs[1] += (x1[0] * x1[1] - x1[2]) * e;
+                gs[2] += (y[0] * y[1] - y[2]) * e;
+            }
+            std::vector<HFr> msg = sc1_message(p.Cc, p.tau[c], gs, L);
+            const size_t m1 = p.proof.b.size();
+            p.proof.u64(msg.size());
+            for (auto& e : msg) p.proof.fr(e);
+            p.T.feed(p.proof.b.data() + m1, p.proof.b.size() - m1);
+            const HFr ch = p.T.rand_fr();
+            p.r_x.push_back(ch);
+            p.Cc = p.Cc * eq1(p.tau[c], ch);
+            for (int m = 0; m < 3; ++m) {
+                std::vector<HFr> nt(half);
+                for (size_t b = 0; b < half; ++b) nt[b] = tabs[m][2 * b] + ch * (tabs[m][2 * b + 1] - tabs[m][2 * b]);
+                tabs[m].swap(nt);
+            }
+        }
+        const HFr v[3] = {tabs[0][0], tabs[1][0], tabs[2][0]};
         // ---- round 4
         size_t m0 = p.proof.b.size();
         for (int m = 0; m < 3; ++m) p.proof.fr(v[m]);
@@ -1859,7 +1902,7 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
     kp_end(I.cols_bytes * k, C.stream);
     // ---- sumcheck 2
     std::vector<Sc2Job> j2(k);
-    for (int i = 1; i <= L; ++i) {
+    for (int i = 1; i <= L - ht; ++i) {
         const uint64_t half = nl >> i;
         const bool fold = i >= 2;
         for (int j = 0; j < k; ++j) {
@@ -1895,6 +1938,47 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
             if (fold) {
                 p.Mc = j2[j].Mout;
                 p.Zc = j2[j].Zout;
+            }
+        }
+    }
+    if (ht > 0) {  // M and Z hold tn entries each: bind r_{L-ht}, then the host rounds
+        {
+            const auto src = each([](P& p) { return Tables3{{const_cast<Fr*>(p.Mc), const_cast<Fr*>(p.Zc), nullptr}}; });
+            const auto dst = each([&](P& p) { return C.pin_dev<Fr>(p.hp); });
+            launch_copy_runs_group(k, src.data(), 2, (int)tn, dst.data(), C.stream);
+        }
+        C.sync();
+        for (auto& p : ps) {
+            const HFr r = p.r_y.back();
+            std::vector<HFr> Mt, Zt;
+            for (uint32_t b = 0; b < tn / 2; ++b) {
+                const HFr m0v = ld_hfr(p.hp + 32 * (2 * b)), m1v = ld_hfr(p.hp + 32 * (2 * b + 1));
+                const HFr z0 = ld_hfr(p.hp + 32 * (tn + 2 * b)), z1 = ld_hfr(p.hp + 32 * (tn + 2 * b + 1));
+                Mt.push_back(m0v + r * (m1v - m0v));
+                Zt.push_back(z0 + r * (z1 - z0));
+            }
+            for (int i = L - ht + 1; i <= L; ++i) {  // prove()'s rounds on gathered tables
+                const size_t half = Mt.size() / 2;
+                HFr q[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
+                for (size_t b = 0; b < half; ++b) {
+                    const HFr m0v = Mt[2 * b], m1v = Mt[2 * b + 1], z0 = Zt[2 * b], z1 = Zt[2 * b + 1];
+                    q[0] += m0v * z0;
+                    q[1] += m1v * z1;
+                    q[2] += (m1v + m1v - m0v) * (z1 + z1 - z0);
+                }
+                const size_t m1 = p.proof.b.size();
+                p.proof.u64(3);
+                for (int t = 0; t < 3; ++t) p.proof.fr(q[t]);
+                p.T.feed(p.proof.b.data() + m1, p.proof.b.size() - m1);
+                const HFr ch = p.T.rand_fr();
+                p.r_y.push_back(ch);
+                std::vector<HFr> nm(half), nz(half);
+                for (size_t b = 0; b < half; ++b) {
+                    nm[b] = Mt[2 * b] + ch * (Mt[2 * b + 1] - Mt[2 * b]);
+                    nz[b] = Zt[2 * b] + ch * (Zt[2 * b + 1] - Zt[2 * b]);
+                }
+                Mt.swap(nm);
+                Zt.swap(nz);
             }
         }
     }

@@ -1347,7 +1347,11 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Tables3 cur{{Az, Bz, Cz}};
     const Fr* Ecur = E1;
     Fr* Ebuf[2] = {Ea, Eb};
-    for (int i = 1; i <= L - g; ++i) {
+    // unsharded: the last ht1 rounds of each sumcheck on the host, as prove_group (tables <= 64 entries;
+    // one proof at a time 22.5 vs 22.6 ms index-cached, throughput equal: profiles/r05/r05zt_ab_hosttail1.jsonl)
+    const int ht1 = G == 1 ? std::min(kGroupHostTail, L - 1) : 0;
+    const uint32_t tn = 2u << ht1;  // entries per table after the device rounds
+    for (int i = 1; i <= L - g - ht1; ++i) {
         const uint64_t half = nl >> i;
         const bool fold = i >= 2;
         Tables3 out{{nullptr, nullptr, nullptr}};
@@ -1393,27 +1397,33 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             if (Eout) Ecur = Eout;
         }
     }
-    // local tables now hold 2 entries each (folded up to r_{L-g-1}); bind r_{L-g} on the host
+    // local tables now hold tn entries each (2 when sharded; folded up to r_{L-g-ht1-1}); bind r_{L-g-ht1}
+    // on the host
     HFr va, vb, vc;
     {
-        for (int m = 0; m < 3; ++m) SPX_HIP(hipMemcpyAsync(hp + 64 * m, cur.t[m], 64, hipMemcpyDeviceToHost, C.stream));
+        for (int m = 0; m < 3; ++m)
+            SPX_HIP(hipMemcpyAsync(hp + 32 * tn * m, cur.t[m], 32 * tn, hipMemcpyDeviceToHost, C.stream));
         C.sync();
         const HFr r = r_x.back();
         std::vector<HFr> mine(3);
-        for (int m = 0; m < 3; ++m) {
-            HFr a0 = ld_hfr(hp + 64 * m), a1 = ld_hfr(hp + 64 * m + 32);
-            mine[m] = a0 + r * (a1 - a0);
-        }
         std::vector<HFr> tabs[3];
         if (G == 1) {
-            for (int m = 0; m < 3; ++m) tabs[m] = {mine[m]};
+            for (int m = 0; m < 3; ++m)
+                for (uint32_t b = 0; b < tn / 2; ++b) {
+                    const HFr a0 = ld_hfr(hp + 32 * (tn * m + 2 * b)), a1 = ld_hfr(hp + 32 * (tn * m + 2 * b + 1));
+                    tabs[m].push_back(a0 + r * (a1 - a0));
+                }
         } else {
+            for (int m = 0; m < 3; ++m) {
+                HFr a0 = ld_hfr(hp + 64 * m), a1 = ld_hfr(hp + 64 * m + 32);
+                mine[m] = a0 + r * (a1 - a0);
+            }
             std::vector<HFr> all = allgather_fr(comm, mine);
             for (int m = 0; m < 3; ++m)
                 for (int r2 = 0; r2 < G; ++r2) tabs[m].push_back(all[3 * r2 + m]);
         }
-        // last g rounds on the gathered tables (size 2^g), same message formula
-        for (int i = L - g + 1; i <= L; ++i) {
+        // last g (+ ht1) rounds on the gathered tables (size 2^g, or 2^ht1 unsharded), same message formula
+        for (int i = L - g - ht1 + 1; i <= L; ++i) {
             const size_t half = tabs[0].size() / 2;
             const int c = i - 1;
             HFr gs[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
@@ -1483,7 +1493,7 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     const Fr* Zc = zl;
     Fr* Mb[2] = {M1, M2};
     Fr* Zb[2] = {Z1, Z2};
-    for (int i = 1; i <= L - g; ++i) {
+    for (int i = 1; i <= L - g - ht1; ++i) {
         const uint64_t half = nl >> i;
         const bool fold = i >= 2;
         Fr* Mo = fold ? Mb[i & 1] : nullptr;
@@ -1517,19 +1527,29 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             Zc = Zo;
         }
     }
-    if (g > 0) {
-        SPX_HIP(hipMemcpyAsync(hp, Mc, 64, hipMemcpyDeviceToHost, C.stream));
-        SPX_HIP(hipMemcpyAsync(hp + 64, Zc, 64, hipMemcpyDeviceToHost, C.stream));
+    if (g + ht1 > 0) {
+        SPX_HIP(hipMemcpyAsync(hp, Mc, 32 * tn, hipMemcpyDeviceToHost, C.stream));
+        SPX_HIP(hipMemcpyAsync(hp + 32 * tn, Zc, 32 * tn, hipMemcpyDeviceToHost, C.stream));
         C.sync();
         const HFr r = r_y.back();
-        std::vector<HFr> mine(2);
-        for (int k = 0; k < 2; ++k) {
-            HFr a0 = ld_hfr(hp + 64 * k), a1 = ld_hfr(hp + 64 * k + 32);
-            mine[k] = a0 + r * (a1 - a0);
+        std::vector<HFr> Mt, Zt;
+        if (G == 1) {
+            for (uint32_t b = 0; b < tn / 2; ++b) {
+                const HFr m0v = ld_hfr(hp + 32 * (2 * b)), m1v = ld_hfr(hp + 32 * (2 * b + 1));
+                const HFr z0 = ld_hfr(hp + 32 * (tn + 2 * b)), z1 = ld_hfr(hp + 32 * (tn + 2 * b + 1));
+                Mt.push_back(m0v + r * (m1v - m0v));
+                Zt.push_back(z0 + r * (z1 - z0));
+            }
+        } else {
+            std::vector<HFr> mine(2);
+            for (int k = 0; k < 2; ++k) {
+                HFr a0 = ld_hfr(hp + 64 * k), a1 = ld_hfr(hp + 64 * k + 32);
+                mine[k] = a0 + r * (a1 - a0);
+            }
+            std::vector<HFr> all = allgather_fr(comm, mine);
+            for (int r2 = 0; r2 < G; ++r2) Mt.push_back(all[2 * r2]), Zt.push_back(all[2 * r2 + 1]);
         }
-        std::vector<HFr> all = allgather_fr(comm, mine), Mt, Zt;
-        for (int r2 = 0; r2 < G; ++r2) Mt.push_back(all[2 * r2]), Zt.push_back(all[2 * r2 + 1]);
-        for (int i = L - g + 1; i <= L; ++i) {
+        for (int i = L - g - ht1 + 1; i <= L; ++i) {
             const size_t half = Mt.size() / 2;
             HFr ps[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
             for (size_t b = 0; b < half; ++b) {

@@ -1347,9 +1347,13 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     Tables3 cur{{Az, Bz, Cz}};
     const Fr* Ecur = E1;
     Fr* Ebuf[2] = {Ea, Eb};
-    // unsharded: the last ht1 rounds of each sumcheck on the host, as prove_group (tables <= 64 entries;
-    // one proof at a time 22.5 vs 22.6 ms index-cached, throughput equal: profiles/r05/r05zt_ab_hosttail1.jsonl)
-    const int ht1 = G == 1 ? std::min(kGroupHostTail, L - 1) : 0;
+    // The last ht1 rounds of each sumcheck run on the host, as in prove_group: each rank binds its local
+    // tables (<= 64 entries) and, sharded, the ranks' tables are gathered in rank order (the g high
+    // variables) before the last g + ht1 rounds. Unsharded: one proof at a time 22.5 vs 22.6 ms
+    // index-cached, throughput equal (profiles/r05/r05zt_ab_hosttail1.jsonl); a rank of an 8-rank proof
+    // +2.3% (r05zu_ab_shardtail_G8.jsonl: 10 fewer launches and exchanges per proof). Fixed, so every
+    // rank of a communicator agrees.
+    const int ht1 = std::max(0, std::min(kGroupHostTail, L - g - 1));
     const uint32_t tn = 2u << ht1;  // entries per table after the device rounds
     for (int i = 1; i <= L - g - ht1; ++i) {
         const uint64_t half = nl >> i;
@@ -1405,23 +1409,20 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             SPX_HIP(hipMemcpyAsync(hp + 32 * tn * m, cur.t[m], 32 * tn, hipMemcpyDeviceToHost, C.stream));
         C.sync();
         const HFr r = r_x.back();
-        std::vector<HFr> mine(3);
-        std::vector<HFr> tabs[3];
-        if (G == 1) {
-            for (int m = 0; m < 3; ++m)
-                for (uint32_t b = 0; b < tn / 2; ++b) {
-                    const HFr a0 = ld_hfr(hp + 32 * (tn * m + 2 * b)), a1 = ld_hfr(hp + 32 * (tn * m + 2 * b + 1));
-                    tabs[m].push_back(a0 + r * (a1 - a0));
-                }
-        } else {
-            for (int m = 0; m < 3; ++m) {
-                HFr a0 = ld_hfr(hp + 64 * m), a1 = ld_hfr(hp + 64 * m + 32);
-                mine[m] = a0 + r * (a1 - a0);
+        // this rank's tables bound at r: 3 x tn / 2 entries; gathered in rank order (rank = the high
+        // variables), the remaining g + ht1 variables' tables
+        const uint32_t hn = tn / 2;
+        std::vector<HFr> mine(3 * hn);
+        for (int m = 0; m < 3; ++m)
+            for (uint32_t b = 0; b < hn; ++b) {
+                const HFr a0 = ld_hfr(hp + 32 * (tn * m + 2 * b)), a1 = ld_hfr(hp + 32 * (tn * m + 2 * b + 1));
+                mine[m * hn + b] = a0 + r * (a1 - a0);
             }
-            std::vector<HFr> all = allgather_fr(comm, mine);
-            for (int m = 0; m < 3; ++m)
-                for (int r2 = 0; r2 < G; ++r2) tabs[m].push_back(all[3 * r2 + m]);
-        }
+        std::vector<HFr> tabs[3];
+        const std::vector<HFr> all = G == 1 ? mine : allgather_fr(comm, mine);
+        for (int m = 0; m < 3; ++m)
+            for (int r2 = 0; r2 < G; ++r2)
+                for (uint32_t b = 0; b < hn; ++b) tabs[m].push_back(all[(size_t)3 * hn * r2 + m * hn + b]);
         // last g (+ ht1) rounds on the gathered tables (size 2^g, or 2^ht1 unsharded), same message formula
         for (int i = L - g - ht1 + 1; i <= L; ++i) {
             const size_t half = tabs[0].size() / 2;
@@ -1532,23 +1533,21 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         SPX_HIP(hipMemcpyAsync(hp + 32 * tn, Zc, 32 * tn, hipMemcpyDeviceToHost, C.stream));
         C.sync();
         const HFr r = r_y.back();
-        std::vector<HFr> Mt, Zt;
-        if (G == 1) {
-            for (uint32_t b = 0; b < tn / 2; ++b) {
-                const HFr m0v = ld_hfr(hp + 32 * (2 * b)), m1v = ld_hfr(hp + 32 * (2 * b + 1));
-                const HFr z0 = ld_hfr(hp + 32 * (tn + 2 * b)), z1 = ld_hfr(hp + 32 * (tn + 2 * b + 1));
-                Mt.push_back(m0v + r * (m1v - m0v));
-                Zt.push_back(z0 + r * (z1 - z0));
-            }
-        } else {
-            std::vector<HFr> mine(2);
-            for (int k = 0; k < 2; ++k) {
-                HFr a0 = ld_hfr(hp + 64 * k), a1 = ld_hfr(hp + 64 * k + 32);
-                mine[k] = a0 + r * (a1 - a0);
-            }
-            std::vector<HFr> all = allgather_fr(comm, mine);
-            for (int r2 = 0; r2 < G; ++r2) Mt.push_back(all[2 * r2]), Zt.push_back(all[2 * r2 + 1]);
+        const uint32_t hn = tn / 2;
+        std::vector<HFr> mine(2 * hn);
+        for (uint32_t b = 0; b < hn; ++b) {
+            const HFr m0v = ld_hfr(hp + 32 * (2 * b)), m1v = ld_hfr(hp + 32 * (2 * b + 1));
+            const HFr z0 = ld_hfr(hp + 32 * (tn + 2 * b)), z1 = ld_hfr(hp + 32 * (tn + 2 * b + 1));
+            mine[b] = m0v + r * (m1v - m0v);
+            mine[hn + b] = z0 + r * (z1 - z0);
         }
+        const std::vector<HFr> all = G == 1 ? mine : allgather_fr(comm, mine);
+        std::vector<HFr> Mt, Zt;
+        for (int r2 = 0; r2 < G; ++r2)
+            for (uint32_t b = 0; b < hn; ++b) {
+                Mt.push_back(all[(size_t)2 * hn * r2 + b]);
+                Zt.push_back(all[(size_t)2 * hn * r2 + hn + b]);
+            }
         for (int i = L - g - ht1 + 1; i <= L; ++i) {
             const size_t half = Mt.size() / 2;
             HFr ps[3] = {HFr::zero(), HFr::zero(), HFr::zero()};

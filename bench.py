@@ -1160,9 +1160,19 @@ def c2_line(spx, L, args, B):
     assert pg == proofs[:C2_GROUP]
     rgroup = roofline_hbm(gstats, None)
     if rgroup:
+        # traffic: the group kernel's own PMC pass (profiles/pmc_kernels_c2.json: the C2 profile run proves
+        # its proofs in a group), e.g. k_sc1_wave<...> -> k_sc1_wave_group<...>
+        sym = rgroup["kernel"]
+        gsym = sym.split("<")[0] + "_group" + (sym[sym.index("<"):] if "<" in sym else "")
+        try:
+            gk = json.load(open(PMC_FILE_C2)).get("kernels", {}).get(gsym) or {}
+        except (OSError, ValueError):
+            gk = {}
+        rgroup["traffic"] = gk.get("traffic_bytes_largest")
+        rgroup["traffic_kernel"] = gsym if gk else None
         rgroup["note"] = ("one lockstep group of %d proofs alone: algorithmic bytes of the kernel's largest group "
-                          "launch (all %d proofs) / its HIP-event duration; traffic: no PMC pass of the group "
-                          "kernels" % (C2_GROUP, C2_GROUP))
+                          "launch (all %d proofs) / its HIP-event duration; traffic from the group kernel's PMC "
+                          "passes" % (C2_GROUP, C2_GROUP))
     # the same pipeline with the matrices absorbed once at index time (bit-identical proofs): the GPU
     # side's capacity, which the per-proof host hashing hides in `value`
     t0 = time.perf_counter()

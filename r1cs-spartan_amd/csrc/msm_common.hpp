@@ -18,7 +18,9 @@ uint32_t seg1_len(bool g2);                      // kSeg1Default for both curves
 uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem);
 static constexpr uint32_t kSeg = 4;           // partials per thread, XYZZ accumulation levels (4: shallow levels)
 static constexpr uint32_t kTreeChunkLog = 2;  // buckets per running-sum chunk of the weighting leaf: 4
-static constexpr uint32_t kTopNodes = 16;  // k_tree_top: the levels whose input has <= 16 nodes, one launch
+// k_tree_top: the levels whose input has <= 32 nodes, one launch (one level launch fewer per batch
+// than 16: G = 8 rank +1.0%, N = 1 +1.4%; 64: +0.8% / +0.4%, 147 KB of LDS; profiles/r05/r05zz_ab_topnodes_*.jsonl)
+static constexpr uint32_t kTopNodes = 32;
 static constexpr int kLight = 256;  // threads for bookkeeping kernels
 static constexpr int kHeavy = 64;   // threads for curve kernels (register-heavy)
 

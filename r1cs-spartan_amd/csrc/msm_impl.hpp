@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kHeavy, Acc<F>::kWaves) void k_tree_level(
 }
 
 // The top levels of every instance's weighting tree in ONE launch: one workgroup per instance, its
-// nodes in LDS (the levels whose input has <= kTopNodes nodes; each is 2 dependent additions, so
+// nodes in LDS (the levels whose input has <= kTopNodes = 32 nodes; each is 2 dependent additions, so
 // launching them one by one cost a launch gap per level). Then, for an instance split over the ranks
 // (this rank holds buckets u = sel + G k, G = 2^lg, as local buckets k, and the tree computed
 // F = sum_k (k + 1) X_k, S = sum_k X_k), the rank's share sum_k (sel + G k + 1) X_k = G F - (G - 1 - sel) S;

@@ -16,8 +16,11 @@ static constexpr uint32_t kSeg1Default = 64;  // references per thread, affine a
 uint32_t seg1_len(bool g2);                      // kSeg1Default for both curves
 // seg1 lowered so the accumulation grid fills whole rounds of resident waves (no near-empty last round)
 uint32_t seg1_fit(uint32_t seg1, uint64_t refs, int waves_per_simd, int lanes_per_elem);
-static constexpr uint32_t kSeg = 4;           // partials per thread, XYZZ accumulation levels (4: shallow levels)
-static constexpr uint32_t kTreeChunkLog = 2;  // buckets per running-sum chunk of the weighting leaf: 4
+// partials per thread, XYZZ accumulation levels (4: shallow levels; 8 measured -0.6% for a G = 8 rank,
+// -0.4% at N = 1: profiles/r05/r05zza_ab_seg_chunk_*.jsonl)
+static constexpr uint32_t kSeg = 4;
+// buckets per running-sum chunk of the weighting leaf: 4 (8: within noise, r05zza_ab_seg_chunk_*.jsonl)
+static constexpr uint32_t kTreeChunkLog = 2;
 // k_tree_top: the levels whose input has <= 32 nodes, one launch (one level launch fewer per batch
 // than 16: G = 8 rank +1.0%, N = 1 +1.4%; 64: +0.8% / +0.4%, 147 KB of LDS; profiles/r05/r05zz_ab_topnodes_*.jsonl)
 static constexpr uint32_t kTopNodes = 32;

@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kThreads) void k_sparse3(SparseView3 mv, const Fr* 
 // are stored, never accumulated. No atomics, no counters.
 static constexpr uint32_t kSpmvPer = 4;  // entries per thread per chunk
 DEV void k_spmv_sliced_body(SpmvSlicedView v, const Fr* __restrict__ z, Fr* o0, Fr* o1,
-                                                          Fr* o2, uint64_t entries) {
+                            Fr* o2, uint64_t entries) {
     constexpr uint64_t kChunkE = kThreads * kSpmvPer;
     const uint64_t d = blockIdx.x & 7u, q = blockIdx.x >> 3, Q = gridDim.x >> 3;
     const uint64_t r0 = entries * d / 8, r1 = entries * (d + 1) / 8;
@@ -411,7 +411,7 @@ __global__ void k_sparse_long_finish(const LongRow* __restrict__ rows, int nrows
 // one product per output entry.
 static constexpr int kEqThreads = 1024;
 DEV void k_eq_factors_body(const Fr* __restrict__ r, EqFactors ef,
-                                                           const Fr* __restrict__ scale) {
+                           const Fr* __restrict__ scale) {
     __shared__ Fr A[64], B[128 * 3];
     const int f = blockIdx.x;
     const int k = ef.k[f];
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(kEqThreads) void k_eq_factors(const Fr* __restrict_
 
 // out[i] = lo[(i + base) & mask] * hi[(i + base) >> klo],  i < count
 DEV void k_eq_expand_body(const Fr* __restrict__ lo, const Fr* __restrict__ hi, int klo,
-                                                        uint64_t base, uint64_t count, Fr* __restrict__ out) {
+                          uint64_t base, uint64_t count, Fr* __restrict__ out) {
     const uint64_t mask = (1ull << klo) - 1;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t x = i + base;
@@ -997,7 +997,7 @@ __global__ __launch_bounds__(kThreads) void k_sc2_round(const Fr* __restrict__ M
 // q[b] = r[2b+1] - r[2b];  r'[b] = r[2b] + p * q[b]   ( = r[2b](1-p) + r[2b+1] p )
 // q may be null (fold only: the commitment-stubbed mode evaluates z without quotients)
 DEV void k_open_level_body(const Fr* __restrict__ rin, Fr* __restrict__ rout,
-                                                         Fr* __restrict__ q, const Fr p, uint64_t half) {
+                           Fr* __restrict__ q, const Fr p, uint64_t half) {
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < half; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr a0 = ld_fr(rin + 2 * b), a1 = ld_fr(rin + 2 * b + 1), d, t;
         fe_sub(d, a1, a0);
@@ -1025,7 +1025,7 @@ struct FoldArgs {
 };
 template <int NF>
 DEV void k_open_fold_body(const Fr* __restrict__ rin, Fr* __restrict__ rout, Fr* __restrict__ q,
-                                                        FoldArgs<NF> a, uint64_t nout) {
+                          FoldArgs<NF> a, uint64_t nout) {
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nout; b += (uint64_t)gridDim.x * blockDim.x) {
         Fr v[1 << NF];
 #pragma unroll
@@ -1083,7 +1083,7 @@ DEV void wave_store_1(Fr* __restrict__ dst, const Fr& x, uint4* lds, int lane) {
 }
 template <int NF>
 DEV void k_open_fold_wave_body(const Fr* __restrict__ rin, Fr* __restrict__ rout,
-                                                             Fr* __restrict__ q, FoldArgs<NF> a, uint64_t nout) {
+                               Fr* __restrict__ q, FoldArgs<NF> a, uint64_t nout) {
     static_assert(NF == 2 || NF == 3, "2 or 3 levels");
     __shared__ uint4 lds_all[kThreads / 64][kWaveLdsChunks];
     uint4* lds = lds_all[threadIdx.x >> 6];
@@ -1151,7 +1151,7 @@ struct TailPoints {
     Fr p[kTailMax <= 512 ? 10 : 20];
 };
 DEV void k_open_tail_body(const Fr* __restrict__ rin, Fr* __restrict__ q, uint32_t h0,
-                                                        int nlev, TailPoints pts, Fr* __restrict__ last) {
+                          int nlev, TailPoints pts, Fr* __restrict__ last) {
     __shared__ Fr buf[2 * kTailMax];
     for (uint32_t b = threadIdx.x; b < 2 * h0; b += blockDim.x) buf[b] = ld_fr(rin + b);
     __syncthreads();

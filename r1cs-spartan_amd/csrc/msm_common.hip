@@ -8,8 +8,9 @@
 //    on a single lane). G2 bases of open level i are pre-summed pairs raw[2b] + raw[2b+1],
 //    because open.rs:46 feeds every quotient scalar twice (q_k[x >> 1]); the MSM result is
 //    identical and half the size.
-//  * Signed c-bit digits -> (bucket, reference) pairs written window-major, hipCUB LSD radix sort
-//    on the bucket bits, run boundaries -> per-bucket counts and offsets. References are 32-bit
+//  * Signed c-bit digits -> (bucket, reference) pairs placed in bucket order by a hand-written
+//    two-level counting sort with LDS histograms (k_sort_*: five launches, no global atomic per pair,
+//    no library kernel), which also yields every partial level's offsets. References are 32-bit
 //    point indices with the sign in bit 31. Order inside a bucket is irrelevant: group addition is
 //    exact and commutative, the affine result is unique.
 //  * Proof-sharded ranks split every instance by BUCKET range (MsmShard, kernels.hpp): each rank
@@ -22,8 +23,6 @@
 //  * Bucket weighting sum_j j S_j as a low-depth (F, S, D) tree (msm_impl.hpp).
 // Many MSMs run as one batch (all nv levels of an opening), and nothing in it waits for the host.
 #include "msm_common.hpp"
-
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -68,302 +67,245 @@ DEV uint32_t digit_key(const MsmInst& I, int32_t d) {
 DEV uint32_t digit_ref(const MsmInst& I, uint32_t w, uint64_t j, int32_t d) {
     return (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
 }
-
-// One thread per scalar. Dense: a (key, reference) pair for every (scalar, window), window-major
-// within each instance so the stores coalesce; digits that are zero or not this rank's get the key
-// nb and sort last. Compact (proof-sharded ranks): only this rank's digits, appended through a
-// block-level scan and one atomic per block (st[1]); pairs past `cap` are dropped and flag st[0].
-// Compact with HIST (the counting sort): each kept digit also takes its rank inside its bucket from
-// the bucket's counter (hist[key]++, returned into posv); otherwise the last block to finish (ticket
-// st[2]) fills the unused key slots with ~0 (sorts last in the radix sort).
-template <bool COMPACT, bool HIST>
-__global__ __launch_bounds__(kLight) void k_msm_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
-                                                     int ninst, uint64_t total, uint32_t nb, const Fr* __restrict__ scalars,
-                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t cap,
-                                                     uint32_t* __restrict__ st, uint32_t* __restrict__ hist,
-                                                     uint32_t* __restrict__ posv) {
-    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    const bool live = g < total;
-    if (!COMPACT && !live) return;
-    MsmInst I{};
-    uint64_t j = 0;
-    Digits d0;
-    if (live) {
-        const int i = find_slot(prefix, ninst, g);
-        j = g - prefix[i];
-        I = insts[i];
-        Fr m, s;
-        load_vec(m, scalars + I.scalar_off + j);
-        fe_from_mont(s, m);
+// Calls f(key, ref) for every digit of batch scalar g that lands in one of this rank's buckets.
+template <class Fn>
+DEV void for_each_key(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix, int nact,
+                      const Fr* __restrict__ scalars, uint64_t g, Fn&& f) {
+    const int i = find_slot(prefix, nact, g);
+    const uint64_t j = g - prefix[i];
+    const MsmInst I = insts[i];
+    Fr m, sc;
+    load_vec(m, scalars + I.scalar_off + j);
+    fe_from_mont(sc, m);
+    Digits d;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d0.s[k] = s.v[k];
-    }
-    if constexpr (!COMPACT) {
-        for (uint32_t w = 0; w < I.W; ++w) {
-            const int32_t d = d0.next(I.c);
-            const uint32_t key = digit_key(I, d);
-            const uint64_t o = I.ref_off + (uint64_t)w * I.size + j;
-            keys[o] = key == ~0u ? nb : key;
-            vals[o] = digit_ref(I, w, j, d);
+    for (int k = 0; k < 8; ++k) d.s[k] = sc.v[k];
+    if (I.c == 16 && I.W == 16) {
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w) {
+            const int32_t dg = d.at16(w);
+            const uint32_t key = digit_key(I, dg);
+            if (key != ~0u) f(key, digit_ref(I, w, j, dg));
         }
     } else {
-        // the digits are extracted once: for up to kKeep windows (c >= 16 at the sizes that matter) the
-        // counting pass keeps every window's key and reference in registers (the window loop unrolled,
-        // so the arrays are indexed statically); more windows recompute them in the writing pass
-        constexpr uint32_t kKeep = 16;
-        uint32_t cnt = 0, kkey[kKeep], kref[kKeep], kpos[kKeep];
-        if (live && I.c == 16 && I.W == kKeep) {
-            Digits d = d0;
-#pragma unroll
-            for (uint32_t w = 0; w < kKeep; ++w) {
-                const int32_t dg = d.at16(w);
-                kkey[w] = digit_key(I, dg);
-                kref[w] = digit_ref(I, w, j, dg);
-                cnt += kkey[w] != ~0u;
-                // independent returning atomics, issued back to back (their latency overlaps)
-                if constexpr (HIST) kpos[w] = kkey[w] != ~0u ? atomicAdd(&hist[kkey[w]], 1u) : 0u;
-            }
-        } else if (live && I.W <= kKeep) {
-            Digits d = d0;
-#pragma unroll
-            for (uint32_t w = 0; w < kKeep; ++w) {
-                kkey[w] = ~0u;
-                if (w < I.W) {
-                    const int32_t dg = d.next(I.c);
-                    kkey[w] = digit_key(I, dg);
-                    kref[w] = digit_ref(I, w, j, dg);
-                }
-                cnt += kkey[w] != ~0u;
-                if constexpr (HIST) kpos[w] = kkey[w] != ~0u ? atomicAdd(&hist[kkey[w]], 1u) : 0u;
-            }
-        } else if (live) {
-            Digits d = d0;
-            for (uint32_t w = 0; w < I.W; ++w) cnt += digit_key(I, d.next(I.c)) != ~0u;
-        }
-        using Scan = hipcub::BlockScan<uint32_t, kLight>;
-        __shared__ typename Scan::TempStorage tmp;
-        __shared__ uint32_t base;
-        __shared__ bool last;
-        uint32_t pre, agg;
-        Scan(tmp).ExclusiveSum(cnt, pre, agg);
-        if (threadIdx.x == 0) {
-            base = agg ? atomicAdd(&st[1], agg) : 0u;
-            if ((uint64_t)base + agg > cap) atomicOr(&st[0], kMsmOverflow);
-        }
-        __syncthreads();
-        if (cnt && I.W <= kKeep) {
-            uint64_t pos = (uint64_t)base + pre;
-#pragma unroll
-            for (uint32_t w = 0; w < kKeep; ++w)
-                if (kkey[w] != ~0u) {
-                    if (pos < cap) {
-                        keys[pos] = kkey[w];
-                        vals[pos] = kref[w];
-                        if constexpr (HIST) posv[pos] = kpos[w];
-                    }
-                    ++pos;
-                }
-        } else if (cnt) {
-            uint64_t pos = (uint64_t)base + pre;
-            Digits d = d0;
-            for (uint32_t w = 0; w < I.W; ++w) {
-                const int32_t dg = d.next(I.c);
-                const uint32_t key = digit_key(I, dg);
-                if (key == ~0u) continue;
-                const uint32_t rk = HIST ? atomicAdd(&hist[key], 1u) : 0u;
-                if (pos < cap) {
-                    keys[pos] = key;
-                    vals[pos] = digit_ref(I, w, j, dg);
-                    if constexpr (HIST) posv[pos] = rk;
-                }
-                ++pos;
-            }
-        }
-        if constexpr (HIST) return;  // the counting sort places the pairs itself: no fillers
-        if (threadIdx.x == 0)  // (its cursor add has returned: every block's slots are taken when the last ticket is)
-            last = atomicAdd(&st[2], 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (last) {  // every block has taken its slots: fill the rest
-            const uint32_t used = min(atomicAdd(&st[1], 0u), cap);
-            for (uint32_t i = used + threadIdx.x; i < cap; i += blockDim.x) keys[i] = ~0u;
+        for (uint32_t w = 0; w < I.W; ++w) {
+            const int32_t dg = d.next(I.c);
+            const uint32_t key = digit_key(I, dg);
+            if (key != ~0u) f(key, digit_ref(I, w, j, dg));
         }
     }
 }
 
-// ------------------------------------------------------------------ counting sort (compacted batches)
-// A proof-sharded rank keeps 1/G of the digits (G = 8 at 2^20: ~2 M pairs per batch into 2^12..2^16
-// local buckets). Their order is: keys pass (hist[key]++ gives each pair its rank in its bucket) ->
-// ONE workgroup derives every offset array from the counts -> one scatter pass. Three launches, no
-// device-wide look-back scans, no fill kernels; the radix sort stays for dense batches and for
-// 2-rank sharding (MsmPlan::counting).
-static constexpr int kScanThreads = 1024;
-static constexpr int kMaxLev = 8;
+// ------------------------------------------------------------------ the bucket sort (hand-written)
+// The (bucket, reference) pairs of a batch are placed in bucket order by a two-level counting sort
+// whose every histogram lives in LDS; no global atomic is taken per pair (per-lane global atomics to
+// scattered words run at ~0.08 TB/s on this chip, MI355X_MICROARCH.md "Global float atomics"):
+//   bins    = ranges of 2^sb consecutive buckets (the batch's nb buckets in nbin <= kMaxBins bins);
+//   tiles   = ranges of kSortThreads x spt consecutive batch scalars (one workgroup each).
+//   K1 k_sort_count  : per tile, digits -> LDS histogram over bins -> column `tile` of cnt[bin][tile];
+//                      block 0 also zeroes the batch's outputs and status words (no fill launch)
+//   K2 k_sort_scan   : per bin, the exclusive scan of its row over the tiles (in place) and the bin's
+//                      total; the last block to finish scans the totals into binbase and checks the
+//                      capacity (compacted keys of a sharded rank: overflow -> empty buckets, rerun)
+//   K3 k_sort_scatter: per tile, the same digits again; each pair takes its slot binbase[bin] +
+//                      row prefix + an LDS rank and is written (reference, in-bin bucket) to the
+//                      bin-partitioned staging
+//   K4 k_sort_bins   : per bin, an LDS histogram over its <= 256 buckets, their offsets, and every
+//                      partial level's per-bucket counts (they depend on the bucket's global offset,
+//                      which is known here) scanned inside the bin; the references are placed in bucket
+//                      order; the last block scans the bins' partial totals
+//   K5 k_sort_final  : each partial level's offsets += the bin's base.
+// Order inside a bucket follows LDS atomics and may differ between runs: group addition is exact and
+// the affine result unique, so every output is identical.
+static constexpr int kSortThreads = 256;
+static constexpr uint32_t kMaxBins = 8192;  // K1 / K3: one LDS word per bin (32 KB)
+static constexpr int kMaxLev = 8;           // XYZZ partial levels the sort prepares offsets for
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+struct SortGeom {
+    uint32_t nb, sb, nbin;  // buckets; in-bin bits (<= 8); bins = ceil(nb / 2^sb)
+    uint32_t spt, ntile;    // scalars per thread; tiles of kSortThreads x spt scalars
+    uint64_t tot_sc;
+};
+
+// block-wide exclusive scan of one value per thread (kSortThreads threads); agg = the block's total.
+// `sh` holds >= kSortThreads / 64 words of LDS; reusable after the call returns.
+DEV uint32_t block_excl_scan(uint32_t v, uint32_t& agg, uint32_t* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    agg = 0;
+#pragma unroll
+    for (int k = 0; k < kSortThreads / 64; ++k) {
+        const uint32_t t = sh[k];
+        pre += k < w ? t : 0u;
+        agg += t;
+    }
+    __syncthreads();
+    return pre + x - v;
+}
+// hand-off to the launch's last block (cdna_hip_programming.md §6 G16, write-through form, as
+// grid_reduce_last in mle_kernels.hip): thread 0 stores the block's words with agent-scope (sc1)
+// stores, drains them, and takes a ticket; true in every thread of the block that drew the last one
+DEV bool handoff_last(uint32_t* __restrict__ ticket, uint32_t ntickets, bool* flag) {
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *flag = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntickets - 1;
+    }
+    __syncthreads();
+    return *flag;
+}
+DEV void st_agent(uint32_t* p, uint32_t v) { __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV uint32_t ld_agent(const uint32_t* p) { return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_count(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
+                                                             int nact, const Fr* __restrict__ scalars, SortGeom g,
+                                                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ zero_dst,
+                                                             uint32_t zero_words) {
+    extern __shared__ uint32_t h[];  // [nbin]
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) h[b] = 0;
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < zero_words; i += kSortThreads) zero_dst[i] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSortThreads * g.spt + threadIdx.x;
+    for (uint32_t k = 0; k < g.spt; ++k) {
+        const uint64_t gi = t0 + (uint64_t)k * kSortThreads;
+        if (gi >= g.tot_sc) break;
+        for_each_key(insts, prefix, nact, scalars, gi, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> g.sb], 1u); });
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) cnt[(size_t)b * g.ntile + blockIdx.x] = h[b];
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_scan(uint32_t* __restrict__ cnt, SortGeom g, uint32_t* __restrict__ bintot,
+                                                            uint32_t* __restrict__ binbase, uint32_t* __restrict__ ticket,
+                                                            uint32_t cap, uint32_t* __restrict__ st,
+                                                            uint32_t* __restrict__ offs_end) {
+    __shared__ uint32_t sh[kSortThreads / 64];
+    __shared__ bool last;
+    uint32_t* row = cnt + (size_t)blockIdx.x * g.ntile;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < g.ntile; base += kSortThreads) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < g.ntile ? row[i] : 0u;
+        uint32_t agg;
+        const uint32_t e = block_excl_scan(v, agg, sh);
+        if (i < g.ntile) row[i] = carry + e;
+        carry += agg;
+    }
+    if (threadIdx.x == 0) st_agent(bintot + blockIdx.x, carry);
+    if (!handoff_last(ticket, g.nbin, &last)) return;
+    carry = 0;
+    for (uint32_t base = 0; base < g.nbin; base += kSortThreads) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < g.nbin ? ld_agent(bintot + i) : 0u;
+        uint32_t agg;
+        const uint32_t e = block_excl_scan(v, agg, sh);
+        if (i < g.nbin) binbase[i] = carry + e;
+        carry += agg;
+    }
+    if (threadIdx.x == 0) {
+        binbase[g.nbin] = carry;
+        const bool over = carry > cap;
+        if (over) atomicOr(&st[0], kMsmOverflow);
+        *offs_end = over ? 0u : carry;
+        *ticket = 0u;
+    }
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
+                                                               int nact, const Fr* __restrict__ scalars, SortGeom g,
+                                                               const uint32_t* __restrict__ cnt,
+                                                               const uint32_t* __restrict__ binbase,
+                                                               const uint32_t* __restrict__ st,
+                                                               uint32_t* __restrict__ sref, uint8_t* __restrict__ sfine) {
+    if (st[0] & kMsmOverflow) return;  // compacted capacity exceeded: the batch reruns dense
+    extern __shared__ uint32_t pos[];   // [nbin]: this tile's next slot in each bin
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) pos[b] = binbase[b] + cnt[(size_t)b * g.ntile + blockIdx.x];
+    __syncthreads();
+    const uint32_t fmask = (1u << g.sb) - 1;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSortThreads * g.spt + threadIdx.x;
+    for (uint32_t k = 0; k < g.spt; ++k) {
+        const uint64_t gi = t0 + (uint64_t)k * kSortThreads;
+        if (gi >= g.tot_sc) break;
+        for_each_key(insts, prefix, nact, scalars, gi, [&](uint32_t key, uint32_t ref) {
+            const uint32_t p = atomicAdd(&pos[key >> g.sb], 1u);
+            sref[p] = ref;
+            sfine[p] = (uint8_t)(key & fmask);
+        });
+    }
+}
+
+// per bin (one workgroup, one thread per in-bin bucket): bucket offsets, the partial levels' counts
+// (affine level: the seg1-reference thread ranges [o, o + c) meets; XYZZ level l: ceil(previous /
+// kSeg)) scanned inside the bin into lev[l], the bin's totals handed to the last block, which scans
+// them into binpfx[l][bin]; then the bin's references in bucket order
 struct LevPtrs {
     uint32_t* p[kMaxLev + 1];  // [0]: the affine level's partial offsets; [l]: XYZZ level l
 };
-// The offsets kernel runs in ONE workgroup of kScanThreads threads and goes through the counts in
-// tiles of kScanThreads x kScanPer buckets (thread t: kScanPer consecutive buckets). Every array it
-// writes is an exclusive scan of a per-bucket count that follows from the bucket's own reference
-// count c and its offset o: the affine level's partials p = c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0
-// (the seg1-reference thread ranges [o, o + c) meets), and each XYZZ level's segments
-// ceil(previous count / kSeg). So a tile needs two block scans (offsets, then all partial arrays
-// at once as one vector) and the counts are read once.
-static constexpr int kScanPer = 8;
-struct ScanVec {
-    uint32_t v[kMaxLev + 1];
-};
-struct ScanVecSum {
-    DEV ScanVec operator()(const ScanVec& a, const ScanVec& b) const {
-        ScanVec r;
-#pragma unroll
-        for (int k = 0; k <= kMaxLev; ++k) r.v[k] = a.v[k] + b.v[k];
-        return r;
+__global__ __launch_bounds__(kSortThreads) void k_sort_bins(SortGeom g, const uint32_t* __restrict__ binbase,
+                                                            const uint32_t* __restrict__ st, const uint32_t* __restrict__ sref,
+                                                            const uint8_t* __restrict__ sfine, uint32_t* __restrict__ offs,
+                                                            uint32_t* __restrict__ refs, uint32_t seg1, int nlev, LevPtrs lev,
+                                                            uint32_t* __restrict__ binsum, uint32_t* __restrict__ binpfx,
+                                                            uint32_t* __restrict__ ticket) {
+    __shared__ uint32_t h[256], sh[kSortThreads / 64];
+    __shared__ bool last;
+    const uint32_t bin = blockIdx.x, f = threadIdx.x;
+    const uint32_t b0 = bin << g.sb, nbk = min(1u << g.sb, g.nb - b0);
+    const bool over = (st[0] & kMsmOverflow) != 0;
+    const uint32_t base = binbase[bin], n = over ? 0u : binbase[bin + 1] - base;
+    h[f] = 0;
+    __syncthreads();
+    for (uint32_t i = f; i < n; i += kSortThreads) atomicAdd(&h[sfine[base + i]], 1u);
+    __syncthreads();
+    const uint32_t c = f < nbk ? h[f] : 0u;
+    uint32_t agg;
+    const uint32_t o = base + block_excl_scan(c, agg, sh);
+    if (f < nbk) offs[b0 + f] = over ? 0u : o;
+    // the partial levels: counts from (c, o), scanned inside the bin
+    uint32_t v = c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0u;
+    for (int l = 0; l <= nlev; ++l) {
+        if (l) v = (v + kSeg - 1) / kSeg;
+        const uint32_t e = block_excl_scan(v, agg, sh);
+        if (f < nbk) lev.p[l][b0 + f] = e;
+        if (f == 0) st_agent(binsum + (size_t)l * (g.nbin + 1) + bin, agg);
     }
-};
-// hist (nb counts) -> offs (nb + 1), lev.p[0] (partials of seg1-reference thread ranges) and
-// lev.p[1..nlev] (segments of kSeg partials), exactly the arrays scan_partials / scan_segs give the
-// dense path; hist is cleared for the next batch. If the counted pairs exceed the capacity (the
-// compaction dropped some), the batch is flagged kMsmOverflow and every offset is 0: later kernels see
-// empty buckets, never read an unwritten slot, and the driver reruns the batch dense.
-__global__ __launch_bounds__(kScanThreads) void k_msm_offsets(uint32_t* __restrict__ hist, uint32_t nb, uint32_t cap,
-                                                              uint32_t* __restrict__ st, uint32_t* __restrict__ offs,
-                                                              uint32_t seg1, int nlev, LevPtrs lev) {
-    using Red = hipcub::BlockReduce<uint32_t, kScanThreads>;
-    using Scan1 = hipcub::BlockScan<uint32_t, kScanThreads>;
-    using ScanV = hipcub::BlockScan<ScanVec, kScanThreads>;
-    __shared__ union {
-        typename Red::TempStorage r;
-        typename Scan1::TempStorage a;
-        typename ScanV::TempStorage v;
-    } tmp;
-    __shared__ uint32_t s_total;
-    {  // pass 1: the total, to decide overflow before anything is written
-        uint32_t sum = 0;
-        for (uint32_t b = threadIdx.x; b < nb; b += kScanThreads) sum += hist[b];
-        const uint32_t t = Red(tmp.r).Sum(sum);
-        if (threadIdx.x == 0) s_total = t;
-        __syncthreads();
+    __syncthreads();
+    h[f] = o;  // this bucket's next slot
+    __syncthreads();
+    for (uint32_t i = f; i < n; i += kSortThreads) refs[atomicAdd(&h[sfine[base + i]], 1u)] = sref[base + i];
+    if (!handoff_last(ticket, g.nbin, &last)) return;
+    for (int l = 0; l <= nlev; ++l) {
+        uint32_t carry = 0;
+        const uint32_t* src = binsum + (size_t)l * (g.nbin + 1);
+        uint32_t* dst = binpfx + (size_t)l * (g.nbin + 1);
+        for (uint32_t b = 0; b < g.nbin; b += kSortThreads) {
+            const uint32_t i = b + f;
+            const uint32_t x = i < g.nbin ? ld_agent(src + i) : 0u;
+            const uint32_t e = block_excl_scan(x, agg, sh);
+            if (i < g.nbin) dst[i] = carry + e;
+            carry += agg;
+        }
+        if (f == 0) dst[g.nbin] = carry;
     }
-    const bool over = s_total > cap;
-    if (over && threadIdx.x == 0) atomicOr(&st[0], kMsmOverflow);
-    const uint32_t n = nb + 1;  // offs[nb] / lev[l][nb]: the totals
-    uint32_t carry0 = 0;
-    ScanVec carry;
-#pragma unroll
-    for (int l = 0; l <= kMaxLev; ++l) carry.v[l] = 0;
-    for (uint32_t base = 0; base < n; base += kScanThreads * kScanPer) {
-        const uint32_t b0 = base + threadIdx.x * kScanPer;
-        uint32_t c[kScanPer], s = 0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            c[k] = b0 + k < nb ? hist[b0 + k] : 0u;
-            s += c[k];
-        }
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k)
-            if (b0 + k < nb) hist[b0 + k] = 0u;
-        uint32_t e0, agg0;
-        Scan1(tmp.a).ExclusiveSum(s, e0, agg0);
-        __syncthreads();
-        // this thread's partial-array counts, summed per array
-        ScanVec sv;
-#pragma unroll
-        for (int l = 0; l <= kMaxLev; ++l) sv.v[l] = 0;
-        uint32_t o = carry0 + e0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            uint32_t v = c[k] ? (o + c[k] - 1) / seg1 - o / seg1 + 1 : 0u;
-            sv.v[0] += v;
-            for (int l = 1; l <= nlev; ++l) {
-                v = (v + kSeg - 1) / kSeg;
-                sv.v[l] += v;
-            }
-            o += c[k];
-        }
-        ScanVec ev, aggv;
-        ScanV(tmp.v).ExclusiveScan(sv, ev, carry, ScanVecSum(), aggv);  // carry as the initial value
-        __syncthreads();
-        o = carry0 + e0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const uint32_t b = b0 + k;
-            if (b < n) {
-                offs[b] = over ? 0u : o;
-                uint32_t v = c[k] ? (o + c[k] - 1) / seg1 - o / seg1 + 1 : 0u;
-                lev.p[0][b] = over ? 0u : ev.v[0];
-                ev.v[0] += v;
-                for (int l = 1; l <= nlev; ++l) {
-                    v = (v + kSeg - 1) / kSeg;
-                    lev.p[l][b] = over ? 0u : ev.v[l];
-                    ev.v[l] += v;
-                }
-            }
-            o += c[k];
-        }
-        carry0 += agg0;
-        carry = ScanVecSum()(carry, aggv);
-    }
-}
-// compacted pair i -> refs[offs[key] + its rank in the bucket] (skipped when the batch overflowed)
-__global__ __launch_bounds__(kLight) void k_msm_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                        const uint32_t* __restrict__ posv, const uint32_t* __restrict__ st,
-                                                        uint32_t cap, const uint32_t* __restrict__ offs,
-                                                        uint32_t* __restrict__ refs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (st[0] & kMsmOverflow) return;
-    if (i >= min(st[1], cap)) return;
-    refs[offs[keys[i]] + posv[i]] = vals[i];
+    if (f == 0) *ticket = 0u;
 }
 
-// sorted keys -> offs[b] = first index with key >= b, for b = 0..nb (offs[nb] = the references;
-// an empty bucket shares the next bucket's offset)
-__global__ __launch_bounds__(kLight) void k_bucket_bounds(const uint32_t* __restrict__ keys, uint64_t n, uint32_t nb,
-                                                          uint32_t* __restrict__ offs) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > nb) return;
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (keys[mid] < b)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    offs[b] = (uint32_t)lo;
-}
-
-// Exclusive offsets of a per-bucket count derived from the previous offsets (device-wide hipCUB
-// scan over a transform iterator: no count array, no extra launch). Counts are off[b + 1] - off[b].
-struct PartialsOp {  // the seg-length thread ranges bucket b's references [off[b], off[b + 1]) meet
-    const uint32_t* off;
-    uint32_t nb, seg;
-    __host__ __device__ uint32_t operator()(uint32_t b) const {
-        if (b >= nb) return 0u;
-        const uint32_t o = off[b], c = off[b + 1] - o;
-        return c ? (o + c - 1) / seg - o / seg + 1 : 0u;
-    }
-};
-struct SegsOp {  // segments of `seg` partials for bucket b's partials [off[b], off[b + 1])
-    const uint32_t* off;
-    uint32_t nb, seg;
-    __host__ __device__ uint32_t operator()(uint32_t b) const {
-        return b < nb ? (off[b + 1] - off[b] + seg - 1) / seg : 0u;
-    }
-};
-template <class Op>
-static void scan_op(MsmWorkspace* ws, const Op& op, uint32_t nb, uint32_t* out, hipStream_t s) {
-    hipcub::CountingInputIterator<uint32_t> cit(0u);
-    hipcub::TransformInputIterator<uint32_t, Op, hipcub::CountingInputIterator<uint32_t>> it(cit, op);
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, it, out, (int)nb + 1, s));
-    void* t = ws->cub.ensure(tb);
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(t, tb, it, out, (int)nb + 1, s));
-}
-void scan_partials(MsmWorkspace* ws, const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np_off, hipStream_t s) {
-    scan_op(ws, PartialsOp{offs, nb, seg}, nb, np_off, s);
-}
-void scan_segs(MsmWorkspace* ws, const uint32_t* off, uint32_t nb, uint32_t seg, uint32_t* seg_off, hipStream_t s) {
-    scan_op(ws, SegsOp{off, nb, seg}, nb, seg_off, s);
+// lev[l][b] += the bin's base; lev[l][nb] = the level's total
+__global__ __launch_bounds__(kSortThreads) void k_sort_final(SortGeom g, int nlev, LevPtrs lev, const uint32_t* __restrict__ binpfx) {
+    const uint64_t t = blockIdx.x * (uint64_t)kSortThreads + threadIdx.x;
+    const uint32_t l = (uint32_t)(t / (g.nb + 1)), b = (uint32_t)(t % (g.nb + 1));
+    if ((int)l > nlev) return;
+    const uint32_t* pf = binpfx + (size_t)l * (g.nbin + 1);
+    lev.p[l][b] = b < g.nb ? lev.p[l][b] + pf[b >> g.sb] : pf[g.nbin];
 }
 
 uint32_t seg1_len(bool) { return kSeg1Default; }
@@ -412,11 +354,6 @@ MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_sc
     while ((1 << g) < G) ++g;
     if ((1 << g) != G || sh.rank < 0 || sh.rank >= G) throw std::runtime_error("MSM shard: bad rank / world");
     o.compact = G > 1 && !sh.dense;
-    // the counting sort for 4 and more ranks (2^20: 2-3.5% more proofs per second than the radix sort
-    // at G = 8, equal at G = 4); at G = 2 a rank keeps half the digits (~8 M pairs per opening batch
-    // into ~10^5 buckets) and the returning bucket atomics and the one-workgroup offsets cost more than
-    // the radix sort does (105 vs 114 M constraints/s): profiles/r05/r05l_*.jsonl, r05m_*.jsonl
-    o.counting = o.compact && G >= 4;
     uint64_t tot_refs = 0;
     double split_refs = 0, whole_refs = 0;
     int nsplit = 0;
@@ -514,68 +451,74 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
     p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
 }
 
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* st, hipStream_t s, uint32_t seg1,
-                   int nlev) {
+// Sort geometry: about 2^kBinsLog bins (in-bin buckets 2^sb <= 256), about 2^kTilesLog tiles.
+static constexpr int kBinsLog = 9, kTilesLog = 9;
+static constexpr size_t kTicketBytes = 128;
+static SortGeom sort_geom(const MsmPlan& p) {
+    SortGeom g;
+    g.nb = p.nb;
+    g.tot_sc = p.tot_sc;
+    int lnb = 0;
+    while ((1ull << lnb) < p.nb) ++lnb;
+    g.sb = (uint32_t)std::min(8, std::max(0, lnb - kBinsLog));
+    g.nbin = (p.nb + (1u << g.sb) - 1) >> g.sb;
+    if (g.nbin > kMaxBins) throw std::runtime_error("MSM batch: too many buckets for the sort");
+    const uint64_t per = (p.tot_sc + (kSortThreads << kTilesLog) - 1) / ((uint64_t)kSortThreads << kTilesLog);
+    g.spt = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, per));
+    const uint64_t ts = (uint64_t)kSortThreads * g.spt;
+    const uint64_t nt = (p.tot_sc + ts - 1) / ts;
+    if (nt > 0x7fffffffull) throw std::runtime_error("MSM batch: too many tiles");
+    g.ntile = (uint32_t)std::max<uint64_t>(1, nt);
+    return g;
+}
+
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, void* out_dev, size_t out_bytes, hipStream_t s,
+                   uint32_t seg1, int nlev) {
+    if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
+    if (out_bytes % 4) throw std::runtime_error("MSM: output bytes not a multiple of 4");
     MsmSorted o;
+    const SortGeom g = sort_geom(p);
     const uint32_t nb = p.nb;
-    const uint64_t n = p.tot_refs;
+    const uint64_t cap = std::max<uint64_t>(p.tot_refs, 1);
+    uint32_t* st = (uint32_t*)((uint8_t*)out_dev + out_bytes - 16);
+    o.offs = (uint32_t*)ws->offs.ensure(4 * (size_t)(nb + 1));
+    o.refs = (uint32_t*)ws->refs.ensure(4 * cap);
+    uint32_t* cnt = (uint32_t*)ws->cnt.ensure(4 * (size_t)g.nbin * g.ntile);
+    uint32_t* bintot = (uint32_t*)ws->bintot.ensure(4 * (size_t)g.nbin);
+    uint32_t* binbase = (uint32_t*)ws->binbase.ensure(4 * (size_t)(g.nbin + 1));
+    // binsum: per level the bins' partial totals; binpfx (after it): their exclusive prefixes
+    uint32_t* binsum = (uint32_t*)ws->binsum.ensure(4 * 2 * (size_t)(kMaxLev + 1) * (g.nbin + 1));
+    uint32_t* binpfx = binsum + (size_t)(kMaxLev + 1) * (g.nbin + 1);
+    uint32_t* sref = (uint32_t*)ws->stage_ref.ensure(4 * cap);
+    uint8_t* sfine = (uint8_t*)ws->stage_fine.ensure(cap);
+    uint32_t* lv = (uint32_t*)ws->lvl.ensure(4 * (size_t)(nb + 1) * (nlev + 1));
+    // two tickets on 64-byte lines of their own: [0] k_sort_scan, [16] k_sort_bins
+    uint32_t* tk = (uint32_t*)ws->tickets.ensure(kTicketBytes);
+    if (!ws->tickets_zeroed) {  // once per workspace: every hand-off's last block resets its ticket
+        HIPCHK(hipMemsetAsync(tk, 0, kTicketBytes, s));
+        ws->tickets_zeroed = true;
+    }
+    LevPtrs lp{};
+    for (int l = 0; l <= nlev; ++l) lp.p[l] = lv + (size_t)l * (nb + 1);
     const int nact = (int)p.insts.size();
-    o.offs = (uint32_t*)ws->offs.ensure(4 * (nb + 1));
-    o.refs = (uint32_t*)ws->refs.ensure(4 * std::max<uint64_t>(n, 1));
-    if (p.counting) {  // counting sort: keys + counts, every offset array in one workgroup, scatter
-        if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
-        uint32_t* hist = (uint32_t*)ws->hist.ensure(4 * (size_t)std::max<uint32_t>(nb, 1));
-        if (ws->hist_zeroed != ws->hist.cap) {  // fresh allocation: zero once; the offsets kernel keeps it zero
-            HIPCHK(hipMemsetAsync(hist, 0, ws->hist.cap, s));
-            ws->hist_zeroed = ws->hist.cap;
-        }
-        uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * std::max<uint64_t>(n, 1));
-        uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
-        uint32_t* pv = (uint32_t*)ws->posv.ensure(4 * std::max<uint64_t>(n, 1));
-        uint32_t* lv = (uint32_t*)ws->lvl.ensure(4 * (size_t)(nb + 1) * (nlev + 1));
-        LevPtrs lp{};
-        for (int l = 0; l <= nlev; ++l) lp.p[l] = lv + (size_t)l * (nb + 1);
-        const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
-        kp_begin(KP_SORT, s);
-        hipLaunchKernelGGL((k_msm_keys<true, true>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc, nb,
-                           scalars, ka, va, (uint32_t)n, st, hist, pv);
-        hipLaunchKernelGGL(k_msm_offsets, dim3(1), dim3(kScanThreads), 0, s, hist, nb, (uint32_t)n, st, o.offs, seg1, nlev,
-                           lp);
-        hipLaunchKernelGGL(k_msm_scatter, dim3((unsigned)((n + kLight - 1) / kLight)), dim3(kLight), 0, s, ka, va, pv, st,
-                           (uint32_t)n, o.offs, o.refs);
-        kp_end(32.0 * p.tot_sc + 4.0 * 6 * n, s);
-        o.np_off = lp.p[0];
-        for (int l = 1; l <= nlev; ++l) o.lev.push_back(lp.p[l]);
-        return o;
-    }
-    // (bucket, reference) pairs, LSD radix sort on the bucket bits, bucket bounds by binary search
-    int bits = 1;
-    while ((1ull << bits) <= nb) ++bits;  // keys 0..nb; the compact filler ~0 has all these bits set
-    uint32_t* ka = (uint32_t*)ws->keys_a.ensure(4 * std::max<uint64_t>(n, 1));
-    uint32_t* kb = (uint32_t*)ws->keys_b.ensure(4 * std::max<uint64_t>(n, 1));
-    uint32_t* va = (uint32_t*)ws->vals_a.ensure(4 * std::max<uint64_t>(n, 1));
-    const int gsc = (int)((p.tot_sc + kLight - 1) / kLight);
-    // (a counting sort, histogram atomics in the keys pass + scan + scatter, measured 10% slower end to
-    // end: profiles/r03/r03t_ab.jsonl; 11-bit onesweep digits no faster: r03at_ab_sort_bits.jsonl)
+    const size_t lds = 4 * (size_t)g.nbin;
     kp_begin(KP_SORT, s);
-    if (p.compact)
-        hipLaunchKernelGGL((k_msm_keys<true, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
-                           nb, scalars, ka, va, (uint32_t)n, st, nullptr, nullptr);
-    else
-        hipLaunchKernelGGL((k_msm_keys<false, false>), dim3(gsc), dim3(kLight), 0, s, p.d_insts, p.d_prefix, nact, p.tot_sc,
-                           nb, scalars, ka, va, 0u, st, nullptr, nullptr);
-    {
-        hipcub::DoubleBuffer<uint32_t> dk(ka, kb), dv(va, o.refs);
-        size_t tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, (int)n, 0, bits, s));
-        void* t = ws->cub.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(t, tb, dk, dv, (int)n, 0, bits, s));
-        o.refs = dv.Current();
-        const uint32_t* sorted = dk.Current();
-        hipLaunchKernelGGL(k_bucket_bounds, dim3((nb + 1 + kLight - 1) / kLight), dim3(kLight), 0, s, sorted, n, nb,
-                           o.offs);
-    }
-    kp_end(32.0 * p.tot_sc + 4.0 * 8 * n, s);
+    hipLaunchKernelGGL(k_sort_count, dim3(g.ntile), dim3(kSortThreads), lds, s, p.d_insts, p.d_prefix, nact, scalars, g, cnt,
+                       (uint32_t*)out_dev, (uint32_t)(out_bytes / 4));
+    hipLaunchKernelGGL(k_sort_scan, dim3(g.nbin), dim3(kSortThreads), 0, s, cnt, g, bintot, binbase, tk, (uint32_t)std::min<uint64_t>(cap, 0xffffffffu),
+                       st, o.offs + nb);
+    hipLaunchKernelGGL(k_sort_scatter, dim3(g.ntile), dim3(kSortThreads), lds, s, p.d_insts, p.d_prefix, nact, scalars, g, cnt,
+                       binbase, st, sref, sfine);
+    hipLaunchKernelGGL(k_sort_bins, dim3(g.nbin), dim3(kSortThreads), 0, s, g, binbase, st, sref, sfine, o.offs, o.refs, seg1,
+                       nlev, lp, binsum, binpfx, tk + 16);
+    const uint64_t nfin = (uint64_t)(nlev + 1) * (nb + 1);
+    hipLaunchKernelGGL(k_sort_final, dim3((unsigned)((nfin + kSortThreads - 1) / kSortThreads)), dim3(kSortThreads), 0, s, g,
+                       nlev, lp, binpfx);
+    // algorithmic bytes: every scalar read twice (32 B), every kept pair staged (5 B), re-read (5 B)
+    // and placed (4 B); the count matrix written, scanned and read (16 B per entry)
+    kp_end(64.0 * p.tot_sc + 14.0 * p.tot_refs + 16.0 * g.nbin * g.ntile, s, (double)p.tot_refs);
+    o.np_off = lp.p[0];
+    for (int l = 1; l <= nlev; ++l) o.lev.push_back(lp.p[l]);
     return o;
 }
 

@@ -1,7 +1,5 @@
 // Shared pieces of the MSM translation units (msm_common.hip, msm_g1.hip, msm_g2.hip).
 #pragma once
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -112,12 +110,13 @@ struct PinArena {
 };
 
 struct MsmWorkspace {
-    DBuf tables, offs, refs, segoff_a, segoff_b, pa, pb, tree_a, tree_b, cub, keys_a, keys_b, vals_a;
-    // compacted (proof-sharded) batches: per-bucket counts (all zero between batches: the offsets
-    // kernel clears what the keys kernel counted), each digit's rank inside its bucket, and the
-    // offset arrays of the affine level and of every XYZZ partial level
-    DBuf hist, posv, lvl;
-    size_t hist_zeroed = 0;  // bytes of `hist` known to be zero
+    DBuf tables, offs, refs, pa, pb, tree_a, tree_b;
+    // bucket sort (msm_sort): per-(bin, tile) counts and their row prefixes, per-bin totals and
+    // bases, the bin-partitioned staging (reference + in-bin bucket), the partial-level offsets and
+    // their per-bin sums / prefixes, and the two hand-off tickets (zero between launches: the last
+    // block of each hand-off resets its ticket)
+    DBuf cnt, bintot, binbase, binsum, stage_ref, stage_fine, lvl, tickets;
+    bool tickets_zeroed = false;
     // compacted-key capacity factor: raised after an overflow, so a workload whose scalars crowd some
     // rank's buckets (e.g. many equal values) stops overflowing after its first batch
     double cap_scale = 1.0;
@@ -133,7 +132,6 @@ struct MsmPlan {
     uint64_t tot_sc = 0;          // scalars digitised
     uint64_t tot_refs = 0;        // key slots: upper bound of the references with a digit in range
     bool compact = false;         // proof-sharded keys (only in-range digits, capacity tot_refs)
-    bool counting = false;        // compacted keys placed by the counting sort (else the radix sort)
     double mu_max = 0;            // largest expected references per bucket over the active instances
     bool any_split = false;
     // weighting tree: per instance, node offset and node count after the chunked leaf; levels above it
@@ -150,25 +148,18 @@ struct MsmPlan {
 MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_scale);
 void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s);
 
-// status words after a batch's outputs (zeroed with them): [0] status bits, [1] compacted-key
-// cursor, [2] keys-kernel ticket
-// Digit / sort stage: sorted (bucket, reference) pairs, per-bucket offsets (offs[nb] = references).
+// status words after a batch's outputs (zeroed with them by the sort's first launch): [0] status bits
+// Digit / sort stage: references sorted by bucket, per-bucket offsets (offs[nb] = references), and
+// the offsets of the affine level's partials (np_off: the seg1-reference thread ranges each bucket
+// meets) and of every planned XYZZ level (lev[l]: segments of kSeg partials per bucket).
 struct MsmSorted {
-    uint32_t *offs, *refs;
-    // compacted batches (counting sort): the partial offsets of the affine level (seg1) and of each
-    // planned XYZZ level, computed in the same launch as offs; null / empty for dense batches, whose
-    // offsets come from scan_partials / scan_segs
-    uint32_t* np_off = nullptr;
+    uint32_t *offs, *refs, *np_off;
     std::vector<uint32_t*> lev;
 };
 // seg1 / nlev: the affine level's references per thread and the number of XYZZ partial levels the
-// driver will run (used by the compacted path, which derives every level's offsets in one launch)
-MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, uint32_t* status_words, hipStream_t s,
+// driver will run. out_dev / out_bytes: the batch's outputs and status words, zeroed by the first
+// launch. Five launches, no host synchronisation, no library kernels (msm_common.hip).
+MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, void* out_dev, size_t out_bytes, hipStream_t s,
                    uint32_t seg1, int nlev);
-// exclusive offsets of the load-balanced affine level's partials per bucket (the seg-length thread
-// ranges a bucket's references [offs[b], offs[b + 1]) meet); np_off[nb] = all partials
-void scan_partials(MsmWorkspace* ws, const uint32_t* offs, uint32_t nb, uint32_t seg, uint32_t* np_off, hipStream_t s);
-// exclusive offsets of the next XYZZ level: segments of `seg` partials per bucket
-void scan_segs(MsmWorkspace* ws, const uint32_t* off, uint32_t nb, uint32_t seg, uint32_t* seg_off, hipStream_t s);
 
 }  // namespace spx

@@ -533,12 +533,13 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     if (ninst <= 0) return;
     const bool g2 = sizeof(F) == sizeof(Fq2);
     const size_t psz = sizeof(Xyzz<F>);
-    // every output starts at infinity (all zero), the status words at 0
-    HIPCHK(hipMemsetAsync(out_dev, 0, msm_out_bytes(g2, ninst), s));
-    uint32_t* st = (uint32_t*)((uint8_t*)out_dev + psz * ninst);
+    const size_t ob = msm_out_bytes(g2, ninst);
     MsmPlan pl = msm_plan(ih, ninst, sh, ws->cap_scale);
     const int nact = (int)pl.insts.size();
-    if (!nact) return;
+    if (!nact) {  // nothing of this batch is this rank's: every output is infinity (all zero), status 0
+        HIPCHK(hipMemsetAsync(out_dev, 0, ob, s));
+        return;
+    }
     msm_upload_plan(ws, pl, s);
     const uint32_t nb = pl.nb;
     const uint64_t tot_refs = pl.tot_refs;
@@ -551,17 +552,13 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     int nlev = 0;
     for (uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1; m > 1; m = (m + kSeg - 1) / kSeg)
         ++nlev;  // partials per bucket, divided by kSeg per level
-    MsmSorted so = msm_sort(ws, pl, scalars, st, s, kSeg1, nlev);
+    // the sort's first launch zeroes the outputs (infinity) and the status words
+    MsmSorted so = msm_sort(ws, pl, scalars, out_dev, ob, s, kSeg1, nlev);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;
     auto* PA = (Xyzz<F>*)ws->pa.ensure(psz * max_segs);
     auto* PB = (Xyzz<F>*)ws->pb.ensure(psz * (max_segs / kSeg + nb + 1));
     uint32_t* cur_off = so.np_off;
     uint32_t* nxt_off = nullptr;
-    if (!cur_off) {  // dense batch: device-wide scans
-        cur_off = (uint32_t*)ws->segoff_a.ensure(4 * (nb + 1));
-        nxt_off = (uint32_t*)ws->segoff_b.ensure(4 * (nb + 1));
-        scan_partials(ws, so.offs, nb, kSeg1, cur_off, s);
-    }
     const uint64_t nthr = (tot_refs + kSeg1 - 1) / kSeg1;
     kp_begin(g2 ? KP_ACC_G2 : KP_ACC_G1, s);
     hipLaunchKernelGGL(k_accum_aff<F>, dim3(acc_blocks<F>(nthr)), dim3(kHeavy), 0, s, so.offs, nb, cur_off, so.refs, pts, PA,
@@ -573,10 +570,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     Xyzz<F>* nxt = PB;
     uint64_t cur_max_segs = max_segs;
     for (int l = 0; l < nlev; ++l) {
-        if (so.np_off)
-            nxt_off = so.lev[l];  // computed with the bucket offsets (counting sort)
-        else
-            scan_segs(ws, cur_off, nb, kSeg, nxt_off, s);
+        nxt_off = so.lev[l];  // computed by the sort
         uint64_t nsegs = cur_max_segs / kSeg + nb + 1;
         kp_begin(g2 ? KP_ACCX_G2 : KP_ACCX_G1, s);
         hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(tree_blocks<F>(nsegs)), dim3(kHeavy), 0, s, nxt_off, nb, cur_off, cur, nxt);

@@ -67,10 +67,15 @@ DEV uint32_t digit_key(const MsmInst& I, int32_t d) {
 DEV uint32_t digit_ref(const MsmInst& I, uint32_t w, uint64_t j, int32_t d) {
     return (uint32_t)(I.pts_off + (uint64_t)w * I.stride + j) | (d < 0 ? 0x80000000u : 0u);
 }
-// Calls f(key, ref) for every digit of batch scalar g that lands in one of this rank's buckets.
+// The digits of batch scalar g that land in one of this rank's buckets. c = 16 with 16 windows (every
+// MSM of >= 2^14 points): all 16 keys and references into registers (unrolled: static indices), so a
+// caller can issue their 16 LDS atomics back to back; otherwise f(key, ref) per digit.
+struct Keys16 {
+    uint32_t key[16], ref[16];  // key ~0u: not this rank's / zero digit
+};
 template <class Fn>
-DEV void for_each_key(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix, int nact,
-                      const Fr* __restrict__ scalars, uint64_t g, Fn&& f) {
+DEV bool scalar_keys(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix, int nact,
+                     const Fr* __restrict__ scalars, uint64_t g, Keys16& k16, Fn&& f) {
     const int i = find_slot(prefix, nact, g);
     const uint64_t j = g - prefix[i];
     const MsmInst I = insts[i];
@@ -84,52 +89,63 @@ DEV void for_each_key(const MsmInst* __restrict__ insts, const uint64_t* __restr
 #pragma unroll
         for (uint32_t w = 0; w < 16; ++w) {
             const int32_t dg = d.at16(w);
-            const uint32_t key = digit_key(I, dg);
-            if (key != ~0u) f(key, digit_ref(I, w, j, dg));
+            k16.key[w] = digit_key(I, dg);
+            k16.ref[w] = digit_ref(I, w, j, dg);
         }
-    } else {
-        for (uint32_t w = 0; w < I.W; ++w) {
-            const int32_t dg = d.next(I.c);
-            const uint32_t key = digit_key(I, dg);
-            if (key != ~0u) f(key, digit_ref(I, w, j, dg));
-        }
+        return true;
     }
+    for (uint32_t w = 0; w < I.W; ++w) {
+        const int32_t dg = d.next(I.c);
+        const uint32_t key = digit_key(I, dg);
+        if (key != ~0u) f(key, digit_ref(I, w, j, dg));
+    }
+    return false;
 }
 
 // ------------------------------------------------------------------ the bucket sort (hand-written)
 // The (bucket, reference) pairs of a batch are placed in bucket order by a two-level counting sort
-// whose every histogram lives in LDS; no global atomic is taken per pair (per-lane global atomics to
-// scattered words run at ~0.08 TB/s on this chip, MI355X_MICROARCH.md "Global float atomics"):
-//   bins    = ranges of 2^sb consecutive buckets (the batch's nb buckets in nbin <= kMaxBins bins);
-//   tiles   = ranges of kSortThreads x spt consecutive batch scalars (one workgroup each).
+// whose histograms live in LDS; no global atomic is taken per pair (per-lane global atomics to
+// scattered words run at ~0.08 TB/s on this chip, MI355X_MICROARCH.md "Global float atomics"), and
+// both scatter passes stage their pairs in LDS so that the global writes are contiguous runs (a wave
+// store to 64 different lines is what bounded the first, unstaged form):
+//   bins    = ranges of 2^sb consecutive buckets (the batch's nb buckets in nbin <= kMaxBins bins),
+//             sized so that a bin's expected pairs fit k_sort_bins's LDS staging;
+//   tiles   = ranges of kTileThreads x spt consecutive batch scalars (one workgroup each).
 //   K1 k_sort_count  : per tile, digits -> LDS histogram over bins -> column `tile` of cnt[bin][tile];
 //                      block 0 also zeroes the batch's outputs and status words (no fill launch)
 //   K2 k_sort_scan   : per bin, the exclusive scan of its row over the tiles (in place) and the bin's
 //                      total; the last block to finish scans the totals into binbase and checks the
 //                      capacity (compacted keys of a sharded rank: overflow -> empty buckets, rerun)
-//   K3 k_sort_scatter: per tile, the same digits again; each pair takes its slot binbase[bin] +
-//                      row prefix + an LDS rank and is written (reference, in-bin bucket) to the
-//                      bin-partitioned staging
+//   K3 k_sort_scatter: per tile, the same digits again, kTileThreads scalars at a time: LDS ranks per
+//                      bin, the pairs ordered by bin in LDS, then written (reference, in-bin bucket)
+//                      as runs at binbase[bin] + row prefix into the bin-partitioned staging
 //   K4 k_sort_bins   : per bin, an LDS histogram over its <= 256 buckets, their offsets, and every
 //                      partial level's per-bucket counts (they depend on the bucket's global offset,
-//                      which is known here) scanned inside the bin; the references are placed in bucket
-//                      order; the last block scans the bins' partial totals
+//                      which is known here) scanned inside the bin; the references ordered by bucket
+//                      in LDS and written back contiguously; the last block scans the bins' partial totals
 //   K5 k_sort_final  : each partial level's offsets += the bin's base.
 // Order inside a bucket follows LDS atomics and may differ between runs: group addition is exact and
 // the affine result unique, so every output is identical.
-static constexpr int kSortThreads = 256;
-static constexpr uint32_t kMaxBins = 8192;  // K1 / K3: one LDS word per bin (32 KB)
-static constexpr int kMaxLev = 8;           // XYZZ partial levels the sort prepares offsets for
+static constexpr int kTileThreads = 1024;     // K1, K3: one workgroup per tile
+static constexpr int kRowThreads = 1024;      // K2
+static constexpr int kScanThreads = 256;      // K5
+static constexpr int kBinThreads = 1024;      // K4: one workgroup per bin
+static constexpr uint32_t kMaxBins = 2048;    // K1 / K3: LDS words per bin
+static constexpr uint32_t kStagePairs = (uint32_t)kTileThreads * 16;  // K3: one iteration's pairs (<= 16 per scalar)
+static constexpr uint32_t kBinStage = 36864;  // K4: a bin's references ordered in LDS (144 KB); larger bins write directly
+static constexpr int kMaxLev = 8;             // XYZZ partial levels the sort prepares offsets for
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
 struct SortGeom {
     uint32_t nb, sb, nbin;  // buckets; in-bin bits (<= 8); bins = ceil(nb / 2^sb)
-    uint32_t spt, ntile;    // scalars per thread; tiles of kSortThreads x spt scalars
+    uint32_t spt, ntile;    // scalars per thread; tiles of (sub x kCountThreads) x spt scalars
+    uint32_t sub;           // K1 workgroups per tile: kSub (staged form) or 1 (direct form)
     uint64_t tot_sc;
 };
 
-// block-wide exclusive scan of one value per thread (kSortThreads threads); agg = the block's total.
-// `sh` holds >= kSortThreads / 64 words of LDS; reusable after the call returns.
+// block-wide exclusive scan of one value per thread (NT threads); agg = the block's total.
+// `sh` holds >= NT / 64 words of LDS; reusable after the call returns.
+template <int NT>
 DEV uint32_t block_excl_scan(uint32_t v, uint32_t& agg, uint32_t* sh) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
@@ -143,7 +159,7 @@ DEV uint32_t block_excl_scan(uint32_t v, uint32_t& agg, uint32_t* sh) {
     uint32_t pre = 0;
     agg = 0;
 #pragma unroll
-    for (int k = 0; k < kSortThreads / 64; ++k) {
+    for (int k = 0; k < NT / 64; ++k) {
         const uint32_t t = sh[k];
         pre += k < w ? t : 0u;
         agg += t;
@@ -165,49 +181,63 @@ DEV bool handoff_last(uint32_t* __restrict__ ticket, uint32_t ntickets, bool* fl
 DEV void st_agent(uint32_t* p, uint32_t v) { __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DEV uint32_t ld_agent(const uint32_t* p) { return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_count(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
-                                                             int nact, const Fr* __restrict__ scalars, SortGeom g,
-                                                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ zero_dst,
-                                                             uint32_t zero_words) {
-    extern __shared__ uint32_t h[];  // [nbin]
-    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) h[b] = 0;
+// K1 runs kSub workgroups of kCountThreads per tile (more, smaller workgroups than K3's: K1 is the
+// digit extraction alone); sub-unit u counts scalars [u, u + 1) x kCountThreads x spt, so the kSub
+// sub-units of tile t cover exactly its scalars, and column kSub t of a scanned row is the tile's prefix
+static constexpr int kCountThreads = 256, kSub = kTileThreads / kCountThreads;
+static constexpr int kDirectThreads = kCountThreads;  // K3 / K4 of the direct form
+__global__ __launch_bounds__(kCountThreads) void k_sort_count(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
+                                                              int nact, const Fr* __restrict__ scalars, SortGeom g,
+                                                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ zero_dst,
+                                                              uint32_t zero_words) {
+    __shared__ uint32_t h[kMaxBins];
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kCountThreads) h[b] = 0;
     if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < zero_words; i += kSortThreads) zero_dst[i] = 0;
+        for (uint32_t i = threadIdx.x; i < zero_words; i += kCountThreads) zero_dst[i] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * kSortThreads * g.spt + threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kCountThreads * g.spt + threadIdx.x;
     for (uint32_t k = 0; k < g.spt; ++k) {
-        const uint64_t gi = t0 + (uint64_t)k * kSortThreads;
+        const uint64_t gi = t0 + (uint64_t)k * kCountThreads;
         if (gi >= g.tot_sc) break;
-        for_each_key(insts, prefix, nact, scalars, gi, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> g.sb], 1u); });
+        Keys16 kk;
+        auto add = [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> g.sb], 1u); };
+        if (scalar_keys(insts, prefix, nact, scalars, gi, kk, add)) {
+#pragma unroll
+            for (int w = 0; w < 16; ++w)
+                if (kk.key[w] != ~0u) add(kk.key[w], 0u);
+        }
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) cnt[(size_t)b * g.ntile + blockIdx.x] = h[b];
+    const uint32_t ncol = g.ntile * g.sub;
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kCountThreads) cnt[(size_t)b * ncol + blockIdx.x] = h[b];
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_scan(uint32_t* __restrict__ cnt, SortGeom g, uint32_t* __restrict__ bintot,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_sort_scan(uint32_t* __restrict__ cnt, SortGeom g, uint32_t* __restrict__ bintot,
                                                             uint32_t* __restrict__ binbase, uint32_t* __restrict__ ticket,
                                                             uint32_t cap, uint32_t* __restrict__ st,
                                                             uint32_t* __restrict__ offs_end) {
-    __shared__ uint32_t sh[kSortThreads / 64];
+    __shared__ uint32_t sh[NT / 64];
     __shared__ bool last;
-    uint32_t* row = cnt + (size_t)blockIdx.x * g.ntile;
+    const uint32_t ncol = g.ntile * g.sub;
+    uint32_t* row = cnt + (size_t)blockIdx.x * ncol;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < g.ntile; base += kSortThreads) {
+    for (uint32_t base = 0; base < ncol; base += NT) {
         const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < g.ntile ? row[i] : 0u;
+        const uint32_t v = i < ncol ? row[i] : 0u;
         uint32_t agg;
-        const uint32_t e = block_excl_scan(v, agg, sh);
-        if (i < g.ntile) row[i] = carry + e;
+        const uint32_t e = block_excl_scan<NT>(v, agg, sh);
+        if (i < ncol) row[i] = carry + e;
         carry += agg;
     }
     if (threadIdx.x == 0) st_agent(bintot + blockIdx.x, carry);
     if (!handoff_last(ticket, g.nbin, &last)) return;
     carry = 0;
-    for (uint32_t base = 0; base < g.nbin; base += kSortThreads) {
+    for (uint32_t base = 0; base < g.nbin; base += NT) {
         const uint32_t i = base + threadIdx.x;
         const uint32_t v = i < g.nbin ? ld_agent(bintot + i) : 0u;
         uint32_t agg;
-        const uint32_t e = block_excl_scan(v, agg, sh);
+        const uint32_t e = block_excl_scan<NT>(v, agg, sh);
         if (i < g.nbin) binbase[i] = carry + e;
         carry += agg;
     }
@@ -220,77 +250,208 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scan(uint32_t* __restrict
     }
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
+// K3. Per iteration (kTileThreads scalars, one per thread): every c = 16 scalar's <= 16 pairs take an
+// LDS rank in their bin (lcnt), the counts are scanned over the bins (lst = this iteration's run
+// start of each bin), the pairs are placed in bin order in LDS (sk, sr), and thread i writes pair i
+// to pos[bin] + (i - lst[bin]): consecutive threads, consecutive addresses inside a bin's run. A
+// scalar of another window size writes its pairs directly (pos[bin] atomics) before the runs.
+struct ScatterLds {
+    uint32_t pos[kMaxBins];   // this tile's next global slot in each bin
+    uint32_t lst[kMaxBins];   // this iteration's counts, then run starts
+    uint32_t sk[kStagePairs], sr[kStagePairs];
+    uint32_t sh[kTileThreads / 64];
+};
+__global__ __launch_bounds__(kTileThreads) void k_sort_scatter(const MsmInst* __restrict__ insts, const uint64_t* __restrict__ prefix,
                                                                int nact, const Fr* __restrict__ scalars, SortGeom g,
                                                                const uint32_t* __restrict__ cnt,
                                                                const uint32_t* __restrict__ binbase,
                                                                const uint32_t* __restrict__ st,
                                                                uint32_t* __restrict__ sref, uint8_t* __restrict__ sfine) {
     if (st[0] & kMsmOverflow) return;  // compacted capacity exceeded: the batch reruns dense
-    extern __shared__ uint32_t pos[];   // [nbin]: this tile's next slot in each bin
-    for (uint32_t b = threadIdx.x; b < g.nbin; b += kSortThreads) pos[b] = binbase[b] + cnt[(size_t)b * g.ntile + blockIdx.x];
-    __syncthreads();
-    const uint32_t fmask = (1u << g.sb) - 1;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kSortThreads * g.spt + threadIdx.x;
-    for (uint32_t k = 0; k < g.spt; ++k) {
-        const uint64_t gi = t0 + (uint64_t)k * kSortThreads;
-        if (gi >= g.tot_sc) break;
-        for_each_key(insts, prefix, nact, scalars, gi, [&](uint32_t key, uint32_t ref) {
-            const uint32_t p = atomicAdd(&pos[key >> g.sb], 1u);
-            sref[p] = ref;
-            sfine[p] = (uint8_t)(key & fmask);
-        });
+    __shared__ ScatterLds L;
+    const uint32_t tid = threadIdx.x, fmask = (1u << g.sb) - 1;
+    for (uint32_t b = tid; b < g.nbin; b += kTileThreads) L.pos[b] = binbase[b] + cnt[((size_t)b * g.ntile + blockIdx.x) * kSub];  // (staged form: sub = kSub)
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTileThreads * g.spt + tid;
+    for (uint32_t it = 0; it < g.spt; ++it) {
+        const uint64_t gi = t0 + (uint64_t)it * kTileThreads;
+        if (gi - tid >= g.tot_sc) break;  // block-uniform: no scalar of this iteration is in the batch
+        for (uint32_t b = tid; b < g.nbin; b += kTileThreads) L.lst[b] = 0;
+        __syncthreads();  // (also orders the previous iteration's pos updates before the direct writes)
+        Keys16 kk;
+        bool fast = false;
+        uint32_t rk[16];
+        if (gi < g.tot_sc) {
+            auto direct = [&](uint32_t key, uint32_t ref) {
+                const uint32_t q = atomicAdd(&L.pos[key >> g.sb], 1u);
+                sref[q] = ref;
+                sfine[q] = (uint8_t)(key & fmask);
+            };
+            fast = scalar_keys(insts, prefix, nact, scalars, gi, kk, direct);
+            if (fast) {
+#pragma unroll
+                for (int w = 0; w < 16; ++w) rk[w] = kk.key[w] != ~0u ? atomicAdd(&L.lst[kk.key[w] >> g.sb], 1u) : 0u;
+            }
+        }
+        __syncthreads();
+        // run starts: exclusive scan of the counts over the bins
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < g.nbin; base += kTileThreads) {
+            const uint32_t b = base + tid;
+            const uint32_t v = b < g.nbin ? L.lst[b] : 0u;
+            uint32_t agg;
+            const uint32_t e = block_excl_scan<kTileThreads>(v, agg, L.sh);
+            if (b < g.nbin) L.lst[b] = carry + e;
+            carry += agg;
+        }
+        const uint32_t total = carry;  // this iteration's staged pairs (<= kStagePairs)
+        __syncthreads();
+        if (fast) {
+#pragma unroll
+            for (int w = 0; w < 16; ++w)
+                if (kk.key[w] != ~0u) {
+                    const uint32_t q = L.lst[kk.key[w] >> g.sb] + rk[w];
+                    L.sk[q] = kk.key[w];
+                    L.sr[q] = kk.ref[w];
+                }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < total; i += kTileThreads) {
+            const uint32_t key = L.sk[i], b = key >> g.sb;
+            const uint32_t q = L.pos[b] + (i - L.lst[b]);
+            sref[q] = L.sr[i];
+            sfine[q] = (uint8_t)(key & fmask);
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < g.nbin; b += kTileThreads) {  // advance by this iteration's run lengths
+            const uint32_t e = b + 1 < g.nbin ? L.lst[b + 1] : total;
+            L.pos[b] += e - L.lst[b];
+        }
+        __syncthreads();  // lst is cleared for the next iteration
     }
 }
 
-// per bin (one workgroup, one thread per in-bin bucket): bucket offsets, the partial levels' counts
-// (affine level: the seg1-reference thread ranges [o, o + c) meets; XYZZ level l: ceil(previous /
-// kSeg)) scanned inside the bin into lev[l], the bin's totals handed to the last block, which scans
-// them into binpfx[l][bin]; then the bin's references in bucket order
+// K3, direct form (tiles of kDirectThreads x spt scalars, sub = 1): the pairs of a scalar take their
+// slots from LDS atomics on pos (the 16 returning atomics issued back to back) and are written where
+// they land. Chosen for sparse batches (a sharded rank keeps 1/G of the digits): per bin and tile
+// too few pairs for runs, and the staged form's 144 KB workgroups would hold whole CUs.
+__global__ __launch_bounds__(kDirectThreads) void k_sort_scatter_direct(const MsmInst* __restrict__ insts,
+                                                                        const uint64_t* __restrict__ prefix, int nact,
+                                                                        const Fr* __restrict__ scalars, SortGeom g,
+                                                                        const uint32_t* __restrict__ cnt,
+                                                                        const uint32_t* __restrict__ binbase,
+                                                                        const uint32_t* __restrict__ st,
+                                                                        uint32_t* __restrict__ sref, uint8_t* __restrict__ sfine) {
+    if (st[0] & kMsmOverflow) return;
+    __shared__ uint32_t pos[kMaxBins];
+    for (uint32_t b = threadIdx.x; b < g.nbin; b += kDirectThreads) pos[b] = binbase[b] + cnt[(size_t)b * g.ntile + blockIdx.x];
+    __syncthreads();
+    const uint32_t fmask = (1u << g.sb) - 1;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDirectThreads * g.spt + threadIdx.x;
+    for (uint32_t k = 0; k < g.spt; ++k) {
+        const uint64_t gi = t0 + (uint64_t)k * kDirectThreads;
+        if (gi >= g.tot_sc) break;
+        Keys16 kk;
+        auto put = [&](uint32_t key, uint32_t ref) {
+            const uint32_t q = atomicAdd(&pos[key >> g.sb], 1u);
+            sref[q] = ref;
+            sfine[q] = (uint8_t)(key & fmask);
+        };
+        if (scalar_keys(insts, prefix, nact, scalars, gi, kk, put)) {
+            uint32_t q[16];
+#pragma unroll
+            for (int w = 0; w < 16; ++w) q[w] = kk.key[w] != ~0u ? atomicAdd(&pos[kk.key[w] >> g.sb], 1u) : 0u;
+#pragma unroll
+            for (int w = 0; w < 16; ++w)
+                if (kk.key[w] != ~0u) {
+                    sref[q[w]] = kk.ref[w];
+                    sfine[q[w]] = (uint8_t)(kk.key[w] & fmask);
+                }
+        }
+    }
+}
+
+// K4: per bin (one workgroup): bucket offsets, the partial levels' counts (affine level: the
+// seg1-reference thread ranges [o, o + c) meets; XYZZ level l: ceil(previous / kSeg)) scanned inside
+// the bin into lev[l], the bin's totals handed to the last block, which scans them into
+// binpfx[l][bin]; then the bin's references ordered by bucket in LDS and written back contiguously
+// (a bin larger than the staging: each reference written to its slot directly)
+template <int NT, uint32_t STAGE>
+struct BinLds {
+    uint32_t out[STAGE ? STAGE : 1];
+    uint32_t h[256], sh[NT / 64];
+};
 struct LevPtrs {
     uint32_t* p[kMaxLev + 1];  // [0]: the affine level's partial offsets; [l]: XYZZ level l
 };
-__global__ __launch_bounds__(kSortThreads) void k_sort_bins(SortGeom g, const uint32_t* __restrict__ binbase,
+// NT threads (>= 256: one per in-bin bucket); STAGE: LDS staging capacity (0: every reference written directly)
+template <int NT, uint32_t STAGE>
+__global__ __launch_bounds__(NT) void k_sort_bins(SortGeom g, const uint32_t* __restrict__ binbase,
                                                             const uint32_t* __restrict__ st, const uint32_t* __restrict__ sref,
                                                             const uint8_t* __restrict__ sfine, uint32_t* __restrict__ offs,
                                                             uint32_t* __restrict__ refs, uint32_t seg1, int nlev, LevPtrs lev,
                                                             uint32_t* __restrict__ binsum, uint32_t* __restrict__ binpfx,
                                                             uint32_t* __restrict__ ticket) {
-    __shared__ uint32_t h[256], sh[kSortThreads / 64];
+    __shared__ BinLds<NT, STAGE> L;
     __shared__ bool last;
     const uint32_t bin = blockIdx.x, f = threadIdx.x;
     const uint32_t b0 = bin << g.sb, nbk = min(1u << g.sb, g.nb - b0);
     const bool over = (st[0] & kMsmOverflow) != 0;
     const uint32_t base = binbase[bin], n = over ? 0u : binbase[bin + 1] - base;
-    h[f] = 0;
+    // the bin's pairs read as aligned quads: element e of quad q is pair a0 + 4 q + e, valid in
+    // [head, head + n) (the staging buffers have 16 bytes of slack past their capacity)
+    const uint32_t a0 = base & ~3u, head = base - a0, nq = (head + n + 3) / 4;
+    if (f < 256) L.h[f] = 0;
     __syncthreads();
-    for (uint32_t i = f; i < n; i += kSortThreads) atomicAdd(&h[sfine[base + i]], 1u);
+    for (uint32_t q = f; q < nq; q += NT) {
+        const uint32_t w4 = *(const uint32_t*)(sfine + a0 + 4 * q);
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e)
+            if (4 * q + e - head < n) atomicAdd(&L.h[(w4 >> (8 * e)) & 0xFFu], 1u);
+    }
     __syncthreads();
-    const uint32_t c = f < nbk ? h[f] : 0u;
+    const uint32_t c = f < nbk ? L.h[f] : 0u;
     uint32_t agg;
-    const uint32_t o = base + block_excl_scan(c, agg, sh);
+    const uint32_t lo = block_excl_scan<NT>(c, agg, L.sh);  // in-bin offset of bucket f
+    const uint32_t o = base + lo;
     if (f < nbk) offs[b0 + f] = over ? 0u : o;
     // the partial levels: counts from (c, o), scanned inside the bin
     uint32_t v = c ? (o + c - 1) / seg1 - o / seg1 + 1 : 0u;
     for (int l = 0; l <= nlev; ++l) {
         if (l) v = (v + kSeg - 1) / kSeg;
-        const uint32_t e = block_excl_scan(v, agg, sh);
+        const uint32_t e = block_excl_scan<NT>(v, agg, L.sh);
         if (f < nbk) lev.p[l][b0 + f] = e;
         if (f == 0) st_agent(binsum + (size_t)l * (g.nbin + 1) + bin, agg);
     }
+    const bool staged = n <= STAGE;
+    if (f < 256) L.h[f] = staged ? lo : o;  // each bucket's next slot (in LDS / in refs)
     __syncthreads();
-    h[f] = o;  // this bucket's next slot
-    __syncthreads();
-    for (uint32_t i = f; i < n; i += kSortThreads) refs[atomicAdd(&h[sfine[base + i]], 1u)] = sref[base + i];
+    for (uint32_t q = f; q < nq; q += NT) {
+        const uint32_t w4 = *(const uint32_t*)(sfine + a0 + 4 * q);
+        const uint4 r4 = *(const uint4*)(sref + a0 + 4 * q);
+        const uint32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e)
+            if (4 * q + e - head < n) {
+                const uint32_t slot = atomicAdd(&L.h[(w4 >> (8 * e)) & 0xFFu], 1u);
+                if (staged)
+                    L.out[slot] = rr[e];
+                else
+                    refs[slot] = rr[e];
+            }
+    }
+    if (staged) {
+        __syncthreads();
+        for (uint32_t i = f; i < n; i += NT) refs[base + i] = L.out[i];
+    }
     if (!handoff_last(ticket, g.nbin, &last)) return;
     for (int l = 0; l <= nlev; ++l) {
         uint32_t carry = 0;
         const uint32_t* src = binsum + (size_t)l * (g.nbin + 1);
         uint32_t* dst = binpfx + (size_t)l * (g.nbin + 1);
-        for (uint32_t b = 0; b < g.nbin; b += kSortThreads) {
+        for (uint32_t b = 0; b < g.nbin; b += NT) {
             const uint32_t i = b + f;
             const uint32_t x = i < g.nbin ? ld_agent(src + i) : 0u;
-            const uint32_t e = block_excl_scan(x, agg, sh);
+            const uint32_t e = block_excl_scan<NT>(x, agg, L.sh);
             if (i < g.nbin) dst[i] = carry + e;
             carry += agg;
         }
@@ -299,9 +460,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_bins(SortGeom g, const ui
     if (f == 0) *ticket = 0u;
 }
 
-// lev[l][b] += the bin's base; lev[l][nb] = the level's total
-__global__ __launch_bounds__(kSortThreads) void k_sort_final(SortGeom g, int nlev, LevPtrs lev, const uint32_t* __restrict__ binpfx) {
-    const uint64_t t = blockIdx.x * (uint64_t)kSortThreads + threadIdx.x;
+// K5: lev[l][b] += the bin's base; lev[l][nb] = the level's total
+__global__ __launch_bounds__(kScanThreads) void k_sort_final(SortGeom g, int nlev, LevPtrs lev, const uint32_t* __restrict__ binpfx) {
+    const uint64_t t = blockIdx.x * (uint64_t)kScanThreads + threadIdx.x;
     const uint32_t l = (uint32_t)(t / (g.nb + 1)), b = (uint32_t)(t % (g.nb + 1));
     if ((int)l > nlev) return;
     const uint32_t* pf = binpfx + (size_t)l * (g.nbin + 1);
@@ -451,24 +612,48 @@ void msm_upload_plan(MsmWorkspace* ws, MsmPlan& p, hipStream_t s) {
     p.d_noff = (uint32_t*)(d + b0 + b1 + b2 + b3);
 }
 
-// Sort geometry: about 2^kBinsLog bins (in-bin buckets 2^sb <= 256), about 2^kTilesLog tiles.
-static constexpr int kBinsLog = 9, kTilesLog = 9;
+// Sort geometry, by the batch's expected pairs per scalar (rho: 16 dense, ~16 / G on a rank of a
+// G-rank proof):
+//  * staged form (rho >= kStagedRho): bins as few as the in-bin staging allows (long runs in K3),
+//    i.e. 2^sb buckets of the batch's most crowded instance expected to fill <= 80% of kBinStage;
+//    tiles of kTileThreads x spt scalars, about 2^8 of them (one workgroup per CU);
+//  * direct form: about 2^9 bins and 2^9 tiles of kDirectThreads x spt scalars.
+// Either way at most kMaxBins bins. SPX_SORT_FORM=staged|direct (A/B) forces a form.
+static constexpr double kStagedRho = 6.0;
 static constexpr size_t kTicketBytes = 128;
-static SortGeom sort_geom(const MsmPlan& p) {
+static int sort_form_env() {  // -1: by rho; 0: direct; 1: staged
+    static const int v = [] {
+        const char* e = getenv("SPX_SORT_FORM");
+        if (!e) return -1;
+        return std::string(e) == "staged" ? 1 : std::string(e) == "direct" ? 0 : -1;
+    }();
+    return v;
+}
+static SortGeom sort_geom(const MsmPlan& p, bool& staged) {
     SortGeom g;
     g.nb = p.nb;
     g.tot_sc = p.tot_sc;
+    const double rho = p.tot_sc ? (double)p.tot_refs / (double)p.tot_sc : 0.0;
+    staged = sort_form_env() >= 0 ? sort_form_env() == 1 : rho >= kStagedRho;
     int lnb = 0;
     while ((1ull << lnb) < p.nb) ++lnb;
-    g.sb = (uint32_t)std::min(8, std::max(0, lnb - kBinsLog));
+    int sb = 8;
+    if (staged)
+        while (sb > 0 && (double)(1u << sb) * std::max(p.mu_max, 1.0) > 0.8 * kBinStage) --sb;
+    else
+        sb = std::min(8, std::max(0, lnb - 9));
+    while (sb < 8 && ((uint64_t)p.nb + (1u << sb) - 1) >> sb > kMaxBins) ++sb;
+    g.sb = (uint32_t)sb;
     g.nbin = (p.nb + (1u << g.sb) - 1) >> g.sb;
     if (g.nbin > kMaxBins) throw std::runtime_error("MSM batch: too many buckets for the sort");
-    const uint64_t per = (p.tot_sc + (kSortThreads << kTilesLog) - 1) / ((uint64_t)kSortThreads << kTilesLog);
-    g.spt = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, per));
-    const uint64_t ts = (uint64_t)kSortThreads * g.spt;
+    const int threads = staged ? kTileThreads : kDirectThreads, tiles_log = staged ? 8 : 9;
+    const uint64_t tile_sc = (uint64_t)threads << tiles_log;
+    g.spt = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (p.tot_sc + tile_sc - 1) / tile_sc));
+    const uint64_t ts = (uint64_t)threads * g.spt;
     const uint64_t nt = (p.tot_sc + ts - 1) / ts;
-    if (nt > 0x7fffffffull) throw std::runtime_error("MSM batch: too many tiles");
+    if (nt > 0x7fffffffull / kSub) throw std::runtime_error("MSM batch: too many tiles");
     g.ntile = (uint32_t)std::max<uint64_t>(1, nt);
+    g.sub = staged ? kSub : 1;
     return g;
 }
 
@@ -477,20 +662,21 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, void* 
     if (nlev > kMaxLev) throw std::runtime_error("MSM: too many partial levels");
     if (out_bytes % 4) throw std::runtime_error("MSM: output bytes not a multiple of 4");
     MsmSorted o;
-    const SortGeom g = sort_geom(p);
+    bool staged = false;
+    const SortGeom g = sort_geom(p, staged);
     const uint32_t nb = p.nb;
     const uint64_t cap = std::max<uint64_t>(p.tot_refs, 1);
     uint32_t* st = (uint32_t*)((uint8_t*)out_dev + out_bytes - 16);
     o.offs = (uint32_t*)ws->offs.ensure(4 * (size_t)(nb + 1));
     o.refs = (uint32_t*)ws->refs.ensure(4 * cap);
-    uint32_t* cnt = (uint32_t*)ws->cnt.ensure(4 * (size_t)g.nbin * g.ntile);
+    uint32_t* cnt = (uint32_t*)ws->cnt.ensure(4 * (size_t)g.nbin * g.ntile * g.sub);
     uint32_t* bintot = (uint32_t*)ws->bintot.ensure(4 * (size_t)g.nbin);
     uint32_t* binbase = (uint32_t*)ws->binbase.ensure(4 * (size_t)(g.nbin + 1));
     // binsum: per level the bins' partial totals; binpfx (after it): their exclusive prefixes
     uint32_t* binsum = (uint32_t*)ws->binsum.ensure(4 * 2 * (size_t)(kMaxLev + 1) * (g.nbin + 1));
     uint32_t* binpfx = binsum + (size_t)(kMaxLev + 1) * (g.nbin + 1);
-    uint32_t* sref = (uint32_t*)ws->stage_ref.ensure(4 * cap);
-    uint8_t* sfine = (uint8_t*)ws->stage_fine.ensure(cap);
+    uint32_t* sref = (uint32_t*)ws->stage_ref.ensure(4 * cap + 16);  // + 16: k_sort_bins reads aligned quads
+    uint8_t* sfine = (uint8_t*)ws->stage_fine.ensure(cap + 16);
     uint32_t* lv = (uint32_t*)ws->lvl.ensure(4 * (size_t)(nb + 1) * (nlev + 1));
     // two tickets on 64-byte lines of their own: [0] k_sort_scan, [16] k_sort_bins
     uint32_t* tk = (uint32_t*)ws->tickets.ensure(kTicketBytes);
@@ -501,22 +687,31 @@ MsmSorted msm_sort(MsmWorkspace* ws, const MsmPlan& p, const Fr* scalars, void* 
     LevPtrs lp{};
     for (int l = 0; l <= nlev; ++l) lp.p[l] = lv + (size_t)l * (nb + 1);
     const int nact = (int)p.insts.size();
-    const size_t lds = 4 * (size_t)g.nbin;
     kp_begin(KP_SORT, s);
-    hipLaunchKernelGGL(k_sort_count, dim3(g.ntile), dim3(kSortThreads), lds, s, p.d_insts, p.d_prefix, nact, scalars, g, cnt,
-                       (uint32_t*)out_dev, (uint32_t)(out_bytes / 4));
-    hipLaunchKernelGGL(k_sort_scan, dim3(g.nbin), dim3(kSortThreads), 0, s, cnt, g, bintot, binbase, tk, (uint32_t)std::min<uint64_t>(cap, 0xffffffffu),
-                       st, o.offs + nb);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(g.ntile), dim3(kSortThreads), lds, s, p.d_insts, p.d_prefix, nact, scalars, g, cnt,
-                       binbase, st, sref, sfine);
-    hipLaunchKernelGGL(k_sort_bins, dim3(g.nbin), dim3(kSortThreads), 0, s, g, binbase, st, sref, sfine, o.offs, o.refs, seg1,
-                       nlev, lp, binsum, binpfx, tk + 16);
+    hipLaunchKernelGGL(k_sort_count, dim3(g.ntile * g.sub), dim3(kCountThreads), 0, s, p.d_insts, p.d_prefix, nact, scalars, g,
+                       cnt, (uint32_t*)out_dev, (uint32_t)(out_bytes / 4));
+    const uint32_t cap32 = (uint32_t)std::min<uint64_t>(cap, 0xffffffffu);
+    if (staged) {
+        hipLaunchKernelGGL(k_sort_scan<kRowThreads>, dim3(g.nbin), dim3(kRowThreads), 0, s, cnt, g, bintot, binbase, tk, cap32,
+                           st, o.offs + nb);
+        hipLaunchKernelGGL(k_sort_scatter, dim3(g.ntile), dim3(kTileThreads), 0, s, p.d_insts, p.d_prefix, nact, scalars, g, cnt,
+                           binbase, st, sref, sfine);
+        hipLaunchKernelGGL((k_sort_bins<kBinThreads, kBinStage>), dim3(g.nbin), dim3(kBinThreads), 0, s, g, binbase, st, sref,
+                           sfine, o.offs, o.refs, seg1, nlev, lp, binsum, binpfx, tk + 16);
+    } else {
+        hipLaunchKernelGGL(k_sort_scan<kDirectThreads>, dim3(g.nbin), dim3(kDirectThreads), 0, s, cnt, g, bintot, binbase, tk,
+                           cap32, st, o.offs + nb);
+        hipLaunchKernelGGL(k_sort_scatter_direct, dim3(g.ntile), dim3(kDirectThreads), 0, s, p.d_insts, p.d_prefix, nact, scalars,
+                           g, cnt, binbase, st, sref, sfine);
+        hipLaunchKernelGGL((k_sort_bins<kDirectThreads, 0>), dim3(g.nbin), dim3(kDirectThreads), 0, s, g, binbase, st, sref,
+                           sfine, o.offs, o.refs, seg1, nlev, lp, binsum, binpfx, tk + 16);
+    }
     const uint64_t nfin = (uint64_t)(nlev + 1) * (nb + 1);
-    hipLaunchKernelGGL(k_sort_final, dim3((unsigned)((nfin + kSortThreads - 1) / kSortThreads)), dim3(kSortThreads), 0, s, g,
+    hipLaunchKernelGGL(k_sort_final, dim3((unsigned)((nfin + kScanThreads - 1) / kScanThreads)), dim3(kScanThreads), 0, s, g,
                        nlev, lp, binpfx);
     // algorithmic bytes: every scalar read twice (32 B), every kept pair staged (5 B), re-read (5 B)
     // and placed (4 B); the count matrix written, scanned and read (16 B per entry)
-    kp_end(64.0 * p.tot_sc + 14.0 * p.tot_refs + 16.0 * g.nbin * g.ntile, s, (double)p.tot_refs);
+    kp_end(64.0 * p.tot_sc + 14.0 * p.tot_refs + 16.0 * g.nbin * g.ntile * g.sub, s, (double)p.tot_refs);
     o.np_off = lp.p[0];
     for (int l = 1; l <= nlev; ++l) o.lev.push_back(lp.p[l]);
     return o;

@@ -583,38 +583,93 @@ def comm_seen(ctx, rank, world):
     return len(ids)
 
 
+def shm_exchange_latency(world):
+    """one shared-memory allgather among `world` CPU processes (tools/shm_latency.py; no GPU): the latency
+    charged to every exchange of a rehearsed rank in the with-exchange variant"""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "shm_latency.py"), "--world", str(world), "--iters", "4000"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError("shm latency measurement failed: %s" % r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+# the with-exchange variants of the largest rehearsal: the measured shm allgather latency, and a
+# pessimistic 50 us per exchange (a futex wake-up on every exchange instead of a spinning peer)
+REHEARSAL_PESSIMISTIC_NS = 50000
+
+
 def run_rehearsal(args, log_n, log_v, P):
-    """N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank (rank 0 of G) of every
-    proof, with no peers: every exchange returns its own contribution (spx_ctx_set_comm_rehearsal), so
-    the rank does a real rank's device and host work for its 1/G of the buckets, blocks and hashing.
-    Every rank of the node does the same on its own GPU, so the node's rate is this rank's proof rate
-    (exchange latency taken as free; the proofs of a rehearsal are not valid and are not checked).
-    Each G runs in a child process of its own (tools/vrank_bench.py --solo), with the settings an N = G
-    rank runs with: inflight_for(G) proofs in flight, lvl0_for(G), hw_queues_for(G) hardware queues and
-    sync_poll_for(G). The children run BEFORE this process creates its own contexts: their streams hold
-    hardware queues too, and 4 of this process's beside a child's 32 oversubscribed the GPU's queues
-    (a G = 8 child measured 377 M constraints/s beside them against 400-403 M alone,
+    """N = 1: rehearsal of a G-GPU node, proof-sharded. This GPU runs ONE rank of every proof at a time,
+    with no peers: every exchange returns its own contribution (spx_ctx_set_comm_rehearsal), so the rank
+    does a real rank's device and host work for its 1/G of the buckets, blocks and hashing. EVERY rank
+    r = 0..G-1 is rehearsed in turn (ranks own different blocks, bucket residues and whole instances),
+    and the node runs at its slowest rank: the node estimate is the MINIMUM over the ranks' proof rates x
+    n (per-rank values and their spread are reported). Exchanges are free in that estimate; for the
+    largest G the slowest rank is run again with every exchange charged the shared-memory allgather
+    latency measured among G CPU processes (tools/shm_latency.py), and with a pessimistic 50 us
+    (over_n1_with_exchange). The proofs of a rehearsal are not valid and are not checked.
+    Each G runs in a child process of its own (tools/vrank_bench.py --solo --ranks all), with the
+    settings an N = G rank runs with: inflight_for(G) proofs in flight, lvl0_for(G), hw_queues_for(G)
+    hardware queues and sync_poll_for(G). The children run BEFORE this process creates its own contexts:
+    their streams hold hardware queues too, and 4 of this process's beside a child's 32 oversubscribed
+    the GPU's queues (a G = 8 child measured 377 M constraints/s beside them against 400-403 M alone,
     profiles/r05/r05y_bench.json, r05z_steps.jsonl)."""
-    rehearsal = {"method": "one rank of a G-rank proof-sharded prove on this GPU, no peers (exchanges free), "
-                 "matrices absorbed per proof (1/G of them by this rank), in a child process "
-                 "(tools/vrank_bench.py --solo) run before the headline; node value = the rank's proof rate x n",
-                 "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "msm_reruns": {}, "device_memory": {}}
-    for G in [int(x) for x in args.rehearse.split(",") if x.strip()]:
+    rehearsal = {"method": "every rank r = 0..G-1 of a G-rank proof-sharded prove on this GPU in turn, no peers, matrices "
+                 "absorbed per proof (1/G of them by the rank), in a child process (tools/vrank_bench.py --solo --ranks "
+                 "all) run before the headline; node value = the slowest rank's proof rate x n",
+                 "proofs_in_flight": {}, "hw_queues": {}, "values": {}, "per_rank": {}, "spread_max_over_min": {},
+                 "msm_reruns": {}, "device_memory": {}}
+    gs = [int(x) for x in args.rehearse.split(",") if x.strip()]
+    gmax = max(gs) if gs else 0
+    lat = None
+    if gmax > 1:
+        try:
+            lat = shm_exchange_latency(gmax)
+        except Exception as e:  # reported, the estimate without exchanges stands
+            rehearsal["exchange_latency_error"] = repr(e)
+        rehearsal["exchange_latency"] = lat
+    for G in gs:
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues_for(G)))
         env.setdefault("SPX_SYNC_POLL_US", str(sync_poll_for(G)))
-        cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo",
-               "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P), "--steps", str(args.steps),
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo", "--ranks", "all",
+               "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P),
+               "--steps", str(min(args.steps, args.rehearse_steps)),
                "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
-        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+        if G == gmax and lat:
+            meas = max(lat["allgather_96B_us"], lat["allgather_384B_us"])
+            cmd += ["--exchange-list", "%d,%d" % (max(1, int(meas * 1e3)), REHEARSAL_PESSIMISTIC_NS)]
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=1200)
         if r.returncode != 0:
             raise RuntimeError("rehearsal G=%d failed: %s" % (G, r.stderr[-2000:]))
         d = json.loads(r.stdout.strip().splitlines()[-1])
         rehearsal["values"][str(G)] = d["node_estimate"]
+        rehearsal["per_rank"][str(G)] = d["per_rank"]
+        rehearsal["spread_max_over_min"][str(G)] = d["node_spread"]
         rehearsal["proofs_in_flight"][str(G)] = d["inflight_per_rank"]
         rehearsal["hw_queues"][str(G)] = hw_queues_for(G)
         rehearsal["msm_reruns"][str(G)] = d["msm_reruns"]
         rehearsal["device_memory"][str(G)] = d.get("device_memory")
+        if d.get("slowest_rank_with_exchange_ns"):
+            rehearsal["slowest_rank_with_exchange_ns"] = {str(G): d["slowest_rank_with_exchange_ns"]}
     return rehearsal
+
+
+T_START = time.perf_counter()
+PHASE = ["start"]
+
+
+def heartbeat(period=30.0):
+    """a progress line on stderr every `period` s (long silent phases: the rehearsal children, the 1-core
+    CPU leg of ~220 s), so a supervisor watching the output sees the run alive"""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period)
+            sys.stderr.write("bench.py: %.0f s, %s\n" % (time.perf_counter() - T_START, PHASE[0]))
+            sys.stderr.flush()
+
+    threading.Thread(target=beat, daemon=True).start()
 
 
 def main():
@@ -629,7 +684,12 @@ def main():
     ap.add_argument("--kind", type=int, default=3, help="3 circuit-3n (distinct witnesses), 0 uniform-3n, 1 ref-shaped")
     ap.add_argument("--witnesses", type=int, default=0, help="distinct witnesses (kind 3; default: one per proof of a step)")
     ap.add_argument("--mode", default="fs", choices=["fs", "injected"])
-    ap.add_argument("--cpu-log-n", type=int, default=16, help="1-core CPU baseline sample size (one proof ~17 s)")
+    ap.add_argument("--cpu-log-n", type=int, default=20,
+                    help="1-core CPU baseline (cpu_baseline) size: the metric's 2^20 by default (one proof, ~220 s, run "
+                    "last; skipped if the run has already taken --cpu-budget-s, the committed record then stands in)")
+    ap.add_argument("--cpu-small-log-n", type=int, default=16, help="extra 1-core sample size (one proof ~17 s)")
+    ap.add_argument("--cpu-budget-s", type=float, default=330.0,
+                    help="wall seconds of the run after which the long 1-core leg is skipped")
     ap.add_argument("--cpu-all-log-n", type=int, default=20,
                     help="all-cores CPU baseline sample size (default: the metric's 2^20, one proof ~30 s on 16 cores)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -647,6 +707,8 @@ def main():
                     "over its group's K GPUs); '' to skip")
     ap.add_argument("--rehearse", default="2,4,8",
                     help="N = 1: world sizes G for the one-rank rehearsal of a G-GPU proof-sharded node ('' to skip)")
+    ap.add_argument("--rehearse-steps", type=int, default=10,
+                    help="steps of P proofs timed per rehearsed rank (at most --steps)")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
                     help="N > 1 headline transport: on-node shared memory (default) or RCCL AllGather (one communicator "
                     "per rank shared by the proofs in flight through the ordered exchange hub; proof groups stay on shm). "
@@ -662,6 +724,7 @@ def main():
     ap.add_argument("--proofs-per-step", type=int, default=64,
                     help="proofs per step (a multiple of --inflight); the K steps run as one pipeline of K x P proofs")
     args = ap.parse_args()
+    heartbeat()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # the driver's `python bench.py --gpus N`: this process becomes the launcher of N ranks
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -695,7 +758,9 @@ def main():
     Bm = max(Bb, Bs, inflight_for(2))
     P = max(Bm, (args.proofs_per_step + Bm - 1) // Bm * Bm)  # proofs per step; each worker proves P / B of them
     # the G-GPU rehearsals first, in child processes, while this process holds no GPU queue (run_rehearsal)
+    PHASE[0] = "rehearsals"
     rehearsal = run_rehearsal(args, log_n, log_v, P) if world == 1 and args.rehearse and not stub else None
+    PHASE[0] = "setup and headline"
     spx = load_product()
     L = spx.lib()
     # SPX_BENCH_SAME_GPU=1: every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)
@@ -799,10 +864,16 @@ def main():
     hctx = hctxs[0]
     # proofs in flight capped by device memory: one probe proof (uncached and index-cached) on the
     # first context measures a context's footprint; every rank keeps the same count (min over ranks)
+    grouped = stub and not sharded_head  # C2: each context proves C2_GROUP proofs in lockstep
+
     def probe():
         for cached in (False, True):
-            spx.MLArgumentForR1CS.prove_witness(hpk, wits[0], pp, mode=args.mode, seed=7, cached=cached,
-                                                commitment_stub=stub)
+            if grouped:  # a group's scratch is ~C2_GROUP times one proof's: probe with one whole group
+                spx.MLArgumentForR1CS.prove_many([hctxs[0]], hpk, [wits[i % W] for i in range(C2_GROUP)], pp,
+                                                 mode=args.mode, seed=7, cached=cached, commitment_stub=stub)
+            else:
+                spx.MLArgumentForR1CS.prove_witness(hpk, wits[0], pp, mode=args.mode, seed=7, cached=cached,
+                                                    commitment_stub=stub)
     nfit, mem_fit = fit_inflight(hctxs, probe)
     if dist is not None:
         import torch
@@ -940,7 +1011,9 @@ def main():
                 del pp_s
                 return b
 
-            one_log_n = args.cpu_log_n if not stub else 16
+            # the 1-core sample at the small size now; the one at the metric's size runs last (run_cpu1)
+            PHASE[0] = "CPU baselines (small sample, all cores)"
+            one_log_n = args.cpu_small_log_n if not stub else 16
             cpu = cpu_baseline(args.kind, one_log_n, log_v, args.cpu_seconds, stub=stub, max_reps=1,
                                pp_bytes=None if stub else gpu_pp_bytes(one_log_n))
             all_log_n = args.cpu_all_log_n if not stub else log_n
@@ -1019,9 +1092,9 @@ def main():
         if world == 1 and log_n == 20 and not stub and args.kind == 3:
             # the headline's baseline at the metric's own size: one core, 2^20 (committed record)
             c1 = committed_record(CPU1_2_20_FILE)
-            if c1:
+            if c1:  # the cross-check of the in-run 1-core 2^20 leg (run last, make_out)
                 c1["gpu_value_over_it"] = round(out["value"] / c1["value"], 1)
-                out["cpu_baseline_1core_2_20"] = c1
+                out["cpu_baseline_1core_2_20_record"] = c1
         c5 = committed_record(C5_FILE)
         if c5 and not stub:
             out["c5_parity_2_24"] = {"equal": c5.get("equal"), "ranks": c5.get("ranks"), "proof_bytes": c5.get("proof_bytes"),
@@ -1057,9 +1130,38 @@ def main():
                 out["ms_per_proof_single_proof_sharded"] = round(ms_o1, 3) if ms_o1 else None
         if rehearsal:
             rehearsal["over_n1"] = {g: round(v / out["value"], 3) for g, v in rehearsal["values"].items()}
+            rehearsal["over_n1_rank0"] = {g: round(pr["0"] / out["value"], 3) for g, pr in rehearsal["per_rank"].items()
+                                          if pr and "0" in pr}
+            if rehearsal.get("slowest_rank_with_exchange_ns"):
+                rehearsal["over_n1_with_exchange"] = {g: {ns: round(v / out["value"], 3) for ns, v in d.items()}
+                                                      for g, d in rehearsal["slowest_rank_with_exchange_ns"].items()}
             out["proof_sharded_rehearsal"] = rehearsal
         if not stub and world == 1 and not args.no_c2:
+            PHASE[0] = "C2 line"
             out["c2"] = c2_line(spx, L, args, args.inflight or C2_INFLIGHT)
+        if cpu is not None:
+            PHASE[0] = "1-core CPU baseline at 2^%d" % args.cpu_log_n
+            # cpu_baseline: one core at the metric's size, timed in this run (last: ~220 s of CPU)
+            out["cpu_baseline_1core_2_%d" % one_log_n] = cpu
+            out["cpu_baseline"] = cpu
+            big = args.cpu_log_n
+            if big != one_log_n and not stub:
+                if time.perf_counter() - T_START > args.cpu_budget_s:
+                    out["cpu_baseline_note"] = ("the 1-core 2^%d leg was skipped: the run had taken %.0f s (> %.0f s); "
+                                                "cpu_baseline is the 2^%d sample, cpu_baseline_1core_2_20 the committed record"
+                                                % (big, time.perf_counter() - T_START, args.cpu_budget_s, one_log_n))
+                else:
+                    p1 = []
+                    c1 = cpu_baseline(args.kind, big, log_v, args.cpu_seconds, max_reps=1, out_proof=p1,
+                                      pp_bytes=pp.serialize_uncompressed() if big == log_n and pp is not None else None)
+                    if big == log_n and args.kind == 3 and args.mode == "fs" and p1:
+                        c1["proof_equals_gpu"] = p1[0] == ref[0]  # the GPU's proof of the same witness
+                    c1["gpu_value_over_it"] = round(out["value"] / c1["value"], 1)
+                    out["cpu_baseline"] = c1
+                    out["cpu_baseline_1core_2_%d" % big] = c1
+                    rec = out.get("cpu_baseline_1core_2_20_record")
+                    if rec and big == 20:
+                        c1["committed_record_value"] = rec["value"]
         return out
 
     out = make_out() if rank == 0 else None
@@ -1193,6 +1295,20 @@ def c2_line(spx, L, args, B):
         "roofline_group": rgroup,
         "hashing_cores_busy": round((hs1[0] - hs0[0]) / el, 2),
     }
+    # the whole pipeline against HBM: the algorithmic bytes of every instrumented launch per proof in the
+    # pipeline's own launch mix (one lockstep group alone: each step of C2_GROUP proofs in one launch, the
+    # SpMV's index streamed once per group), times the proof rate, over 8 TB/s
+    alg = sum(v["bytes"] for v in gstats.values())
+    if alg:
+        rate_c, rate = steps * P / elc, steps * P / el
+        res["hbm_pipeline"] = {
+            "alg_bytes_per_proof": round(alg, 1), "alg_bytes_per_constraint": round(alg / n, 2),
+            "peak_GBs": HBM_PEAK_GBS,
+            "frac_index_cached": round(alg * rate_c / (HBM_PEAK_GBS * 1e9), 4),
+            "frac_per_proof_absorbed": round(alg * rate / (HBM_PEAK_GBS * 1e9), 4),
+            "by_kernel_bytes_per_proof": {k: round(v["bytes"], 1) for k, v in gstats.items()},
+            "note": "algorithmic bytes (kp_end of every launch of one lockstep group alone, per proof) x proofs/s of "
+                    "the pipeline / 8 TB/s; per-proof-absorbed runs at the hashing pool's rate"}
     if not args.no_cpu:
         op = []
         res["cpu_baseline_all_cores"] = cpu_baseline(3, log_n, log_v, args.cpu_seconds, threads=host_cores(), stub=True,

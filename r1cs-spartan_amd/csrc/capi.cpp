@@ -437,7 +437,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     budget = std::max(1, budget);
     // proofs in flight: one per context, or its lockstep group (spx_ctx_set_group) for stubbed proofs
     int nfly = 0;
-    for (int k = 0; k < nctx; ++k) nfly += (base.stub && G == 1) ? std::max(1, ctxs[k]->c->group) : 1;
+    for (int k = 0; k < nctx; ++k) nfly += (base.stub && G == 1) ? std::max(1, ctxs[k]->c->group.load()) : 1;
     const int nbase = std::min(nfly, G >= 4 ? std::max(1, budget / 2) : budget);
     const int lanes = std::max(1, spx::blake2s_lane_width());
     using clk = std::chrono::steady_clock;
@@ -502,7 +502,7 @@ int spx_prove_many(spx_ctx** ctxs, int nctx, spx_pk* idx, spx_witness** wits, in
     };
     auto work = [&](int k) {
         // lockstep groups (spx_ctx_set_group): the context's proofs k, k + nctx, ... in groups of K
-        const int K = ctxs[k]->c->group;
+        const int K = ctxs[k]->c->group.load();
         const bool grouped = K > 1 && base.stub && G == 1;
         std::vector<int> mine;
         for (int i = k; i < nproofs; i += nctx) mine.push_back(i);
@@ -637,6 +637,7 @@ int spx_kernel_ops(spx_ctx* ctx, int id, double* ops) {
 int spx_ctx_set_sync_poll(spx_ctx* ctx, int us) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");
+        if (ctx->c->in_use.load()) spx::invalid("context in use by a prove or session");
         ctx->c->poll_us = us < 0 ? -1 : us;
     });
 }
@@ -644,6 +645,7 @@ int spx_ctx_set_group(spx_ctx* ctx, int k) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");
         if (k < 1 || k > spx::kGroupMax) spx::invalid("lockstep group size must be 1.." + std::to_string(spx::kGroupMax));
+        if (ctx->c->in_use.load()) spx::invalid("context in use by a prove or session");
         ctx->c->group = k;
     });
 }

@@ -1229,9 +1229,41 @@ struct CopyJob {  // up to 3 runs of `per` Fr -> dst, back to back
     const Fr* src[3];
     Fr* dst;
 };
-__global__ __launch_bounds__(kThreads) void k_spmv_sliced_group(SpmvSlicedView v, GroupOf<SpmvJob> g, uint64_t entries) {
-    const SpmvJob& j = g.j[blockIdx.y];
-    k_spmv_sliced_body(v, j.z, j.o[0], j.o[1], j.o[2], entries);
+// The group's SpMVs share one index: each entry (value, column, row | matrix: 40 B) is streamed ONCE
+// and applied to the k proofs' z in turn (gather, product, store per proof), instead of once per
+// proof (blockIdx.y = proof). Same XCD eighths and chunking as k_spmv_sliced_body; per proof the same
+// products land in the same slots, so every proof's Az, Bz, Cz are its own launch's.
+__global__ __launch_bounds__(kThreads) void k_spmv_sliced_group(SpmvSlicedView v, GroupOf<SpmvJob> g, int k,
+                                                                uint64_t entries) {
+    constexpr uint64_t kChunkE = kThreads * kSpmvPer;
+    const uint64_t d = blockIdx.x & 7u, q = blockIdx.x >> 3, Q = gridDim.x >> 3;
+    const uint64_t r0 = entries * d / 8, r1 = entries * (d + 1) / 8;
+    for (uint64_t c0 = r0 + q * kChunkE; c0 < r1; c0 += Q * kChunkE) {
+        uint32_t col[kSpmvPer], dst[kSpmvPer];
+        Fr a[kSpmvPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kSpmvPer; ++j) {
+            const uint64_t i = min(c0 + j * kThreads + threadIdx.x, r1 - 1);
+            col[j] = v.col[i];
+            dst[j] = v.dst[i];
+            a[j] = ld_fr(v.val + i);
+        }
+        for (int p = 0; p < k; ++p) {
+            const SpmvJob& J = g.j[p];
+            Fr zv[kSpmvPer];
+#pragma unroll
+            for (uint32_t j = 0; j < kSpmvPer; ++j) zv[j] = ld_fr(J.z + col[j]);
+#pragma unroll
+            for (uint32_t j = 0; j < kSpmvPer; ++j) {
+                if (c0 + j * kThreads + threadIdx.x < r1) {
+                    Fr t;
+                    fe_mul(t, a[j], zv[j]);
+                    const uint32_t m = dst[j] >> 30, x = dst[j] & 0x3FFFFFFFu;
+                    st_fr((m == 0 ? J.o[0] : (m == 1 ? J.o[1] : J.o[2])) + x, t);
+                }
+            }
+        }
+    }
 }
 __global__ __launch_bounds__(kEqThreads) void k_eq_factors_group(GroupOf<EqfJob> g) {
     const EqfJob& j = g.j[blockIdx.y];
@@ -1556,8 +1588,9 @@ void launch_spmv_sliced_group(int k, const SpmvSlicedView& v, const Fr* const* z
     GroupOf<SpmvJob> g = group_check<SpmvJob>(k);
     for (int i = 0; i < k; ++i) g.j[i] = SpmvJob{z[i], {out[i].t[0], out[i].t[1], out[i].t[2]}};
     const uint64_t per_xcd = (entries / 8 + kThreads * kSpmvPer - 1) / (kThreads * kSpmvPer);
-    const uint32_t Q = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (per_xcd + 1) / 2));
-    hipLaunchKernelGGL(k_spmv_sliced_group, dim3(8 * Q, k), dim3(kThreads), 0, s, v, g, entries);
+    // k proofs per entry: as many workgroups as one proof's launch has, each doing k proofs' products
+    const uint32_t Q = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, per_xcd));
+    hipLaunchKernelGGL(k_spmv_sliced_group, dim3(8 * Q), dim3(kThreads), 0, s, v, g, k, entries);
 }
 void launch_eq_table_group(int k, const Fr* const* r_dev, int nvar, uint64_t base, uint64_t count, Fr* const* out,
                            Fr* const* lo, Fr* const* hi, hipStream_t s) {

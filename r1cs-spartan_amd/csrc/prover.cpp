@@ -56,19 +56,37 @@ static int sync_poll_us() {
     }();
     return v;
 }
-void Ctx::wait_stream(hipStream_t s, hipEvent_t& ev) {
-    const int us = poll_us >= 0 ? poll_us : sync_poll_us();
+void Ctx::wait_stream(hipStream_t s) {
+    const int pu = poll_us.load(std::memory_order_relaxed);
+    const int us = pu >= 0 ? pu : sync_poll_us();
     if (us <= 0) {
         SPX_HIP(hipStreamSynchronize(s));
         return;
     }
-    thread_local bool slack_set = false;
-    if (!slack_set) {  // sleeps of tens of microseconds, not the default 50 us timer slack on top
-        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
-        slack_set = true;
-    }
+    // one event per (thread, device): waits on this context from different threads (a prove worker,
+    // an uploader) never record or query the same event
+    struct TlEvents {
+        std::vector<hipEvent_t> ev;
+        ~TlEvents() {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+        }
+    };
+    thread_local TlEvents tl;
+    if ((int)tl.ev.size() <= device) tl.ev.resize(device + 1, nullptr);
+    hipEvent_t& ev = tl.ev[device];
     if (!ev) SPX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     SPX_HIP(hipEventRecord(ev, s));
+    // sleeps of tens of microseconds, not the default 50 us timer slack on top: the calling thread's
+    // slack is lowered for the poll loop and restored after it
+    const int old_slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+    struct Restore {
+        int v;
+        ~Restore() {
+            if (v > 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)v, 0, 0, 0);
+        }
+    } restore{old_slack};
     for (int i = 0;; ++i) {
         const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return;
@@ -87,8 +105,6 @@ void Ctx::ensure_side() {
 }
 Ctx::~Ctx() {
     (void)hipSetDevice(device);
-    if (wait_ev) (void)hipEventDestroy(wait_ev);
-    if (wait_ev_side) (void)hipEventDestroy(wait_ev_side);
     if (msm_side) msm_ws_destroy(msm_side);
     if (side_ev) (void)hipEventDestroy(side_ev);
     if (side) (void)hipStreamDestroy(side);
@@ -717,7 +733,15 @@ std::unique_ptr<Index> index_build(Ctx& C, const HostCsr* mats) {
     {
         double e_rows = 0;
         for (int m = 0; m < 3; ++m) e_rows += (double)(mats[m].rp[lo + nl] - mats[m].rp[lo]);
-        I->rows_bytes = 68.0 * e_rows + 3.0 * 8.0 * nl + 3.0 * 32.0 * nl;  // 3 outputs
+        if (I->rows_sliced.on) {
+            // column-sorted list: 40 B per entry (value, column, row | matrix), z read once (each XCD
+            // its contiguous eighth), one 32 B output per local row and matrix
+            I->rows_index_bytes = 40.0 * (double)I->rows_sliced.entries;
+            I->rows_bytes = I->rows_index_bytes + 32.0 * n + 3.0 * 32.0 * nl;
+        } else {  // CSR: value + column + a 32 B gather of z per entry, row pointers, 3 outputs
+            I->rows_index_bytes = 36.0 * e_rows + 3.0 * 8.0 * nl;
+            I->rows_bytes = 68.0 * e_rows + 3.0 * 8.0 * nl + 3.0 * 32.0 * nl;
+        }
         // column stream: 32 B value + 4 B row|matrix per entry (eq(r_x) is gathered from its two
         // cache-resident factor tables, not from HBM); 4 B lane word and one 32 B output per column
         I->cols_bytes = 36.0 * (double)I->cols.entries + 4.0 * nl + 32.0 * nl;
@@ -1604,6 +1628,10 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
             (void)hipStreamSynchronize(C.stream);
         }
     } drain{C};
+    // a group records no per-phase marks (its phases interleave k proofs): spx_last_timings reports
+    // its total alone, and the host-phase counters (spx_host_phase_stats) count prove() calls only
+    C.timings.clear();
+    Timer tgroup;
     Comm& comm = *C.comm;
     if (comm.size() != 1 || I.G != 1) invalid("lockstep groups need an unsharded context and index");
     const int L = I.log_n;
@@ -1689,7 +1717,8 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
         const auto zs = each([](P& p) -> const Fr* { return p.z; });
         const auto outs = each([](P& p) { return Tables3{{p.Az, p.Bz, p.Cz}}; });
         launch_spmv_sliced_group(k, I.rows_sliced.view(), zs.data(), outs.data(), I.rows_sliced.entries, C.stream);
-        kp_end(I.rows_bytes * k, C.stream);
+        // one index stream for the group (k_spmv_sliced_group), z and the outputs per proof
+        kp_end(I.rows_index_bytes + (I.rows_bytes - I.rows_index_bytes) * k, C.stream);
     } else {
         for (auto& p : ps)
             launch_sparse3(0, I.rows.view(), p.z, p.Az, p.Bz, p.Cz, nullptr, nl, I.rows.chunks.as<LongChunk>(),
@@ -2009,6 +2038,7 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
     }
     std::vector<std::vector<uint8_t>> out(k);
     for (int j = 0; j < k; ++j) out[j] = std::move(ps[j].proof.b);
+    C.timings.emplace_back("total_group", tgroup.us());
     return out;
 }
 

@@ -3,11 +3,16 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <condition_variable>
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -84,13 +89,27 @@ struct LocalComm : Comm {
 // Rehearsal of ONE rank of a proof-sharded prove on a GPU of its own (bench / scaling estimates):
 // every allgather returns this rank's contribution in all `world` slots, so the rank does exactly a
 // real rank's device and host work without its peers. The proofs it outputs are NOT valid proofs.
+// SPX_REHEARSAL_EXCHANGE_NS (read when the comm is set): each allgather then also takes that long,
+// the latency of a real exchange charged to the rank (bench.py measures it among world CPU processes
+// over the shared-memory transport): a short spin, as comm_shm.cpp's, then a sleep for the rest.
 struct SoloComm : Comm {
     int r, w;
-    SoloComm(int rank, int world) : r(rank), w(world) {}
+    int64_t delay_ns = 0;
+    SoloComm(int rank, int world) : r(rank), w(world) {
+        if (const char* e = getenv("SPX_REHEARSAL_EXCHANGE_NS")) delay_ns = std::max<int64_t>(0, atoll(e));
+    }
     int rank() const override { return r; }
     int size() const override { return w; }
     void allgather(const void* s, void* rv, size_t b) override {
+        const auto t0 = std::chrono::steady_clock::now();
         for (int k = 0; k < w; ++k) memcpy((uint8_t*)rv + k * b, s, b);
+        if (delay_ns <= 0) return;
+        const auto until = t0 + std::chrono::nanoseconds(delay_ns);
+        const auto spin_until = t0 + std::chrono::nanoseconds(std::min<int64_t>(delay_ns, 4000));
+        while (std::chrono::steady_clock::now() < spin_until) {
+        }
+        const auto now = std::chrono::steady_clock::now();
+        if (now < until) std::this_thread::sleep_for(until - now);
     }
 };
 struct GroupState {
@@ -200,21 +219,23 @@ struct Ctx {
     // Waits for a stream's queued work. hipStreamSynchronize under the blocking-sync flag still spins
     // in the HSA runtime before it sleeps (~0.2 ms of a core per wait): with 64 proofs in flight per
     // rank and ~45 waits per proof that spinning was most of a proof's host CPU. With SPX_SYNC_POLL_US
-    // = t > 0 the wait records an event and polls it, sleeping t us between polls (wait_stream).
-    hipEvent_t wait_ev = nullptr, wait_ev_side = nullptr;
-    int poll_us = -1;  // this context's wait: -1 = SPX_SYNC_POLL_US (default 0), 0 = hipStreamSynchronize
+    // = t > 0 the wait records an event of the calling thread's own and polls it, sleeping t us between
+    // polls (wait_stream).
+    // this context's wait: -1 = SPX_SYNC_POLL_US (default 0), 0 = hipStreamSynchronize (atomic: the
+    // setter may run beside a worker's waits; spx_ctx_set_sync_poll refuses a context in use)
+    std::atomic<int> poll_us{-1};
     // spx_prove_many on this context proves its stubbed-commitment, unsharded proofs in lockstep groups
     // of this many (prove_group; 1 = one at a time)
-    int group = 1;
-    void wait_stream(hipStream_t s, hipEvent_t& ev);
+    std::atomic<int> group{1};
+    void wait_stream(hipStream_t s);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
-        wait_stream(stream, wait_ev);
+        wait_stream(stream);
         msm_ws_staging_reset(msm);
         if (kprof.on) kprof.harvest();
     }
     void side_sync() {
         if (!side) return;
-        wait_stream(side, wait_ev_side);
+        wait_stream(side);
         msm_ws_staging_reset(msm_side);
     }
 };
@@ -313,6 +334,7 @@ struct Index {
     bool has_cache = false;
     Blake2s cache;  // transcript state after feeding A, B, C
     double rows_bytes = 0, cols_bytes = 0;  // algorithmic bytes of one SpMV / eval_on_x pass (local)
+    double rows_index_bytes = 0;            // of rows_bytes: the index stream (shared by a lockstep group)
     int G = 1, rank = 0;
 };
 

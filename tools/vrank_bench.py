@@ -32,24 +32,36 @@ def main():
                     "processes have written a ready file into this directory, so their timed regions overlap")
     ap.add_argument("--sync-n", type=int, default=1)
     ap.add_argument("--solo", action="store_true",
-                    help="rehearsal: only rank 0 of the G, without peers (spx_ctx_set_comm_rehearsal), the GPU to "
-                    "itself: value x G estimates an N = G node (exchanges free); its proofs are not valid")
+                    help="rehearsal: one rank of the G, without peers (spx_ctx_set_comm_rehearsal), the GPU to "
+                    "itself: its proof rate x n estimates an N = G node; its proofs are not valid")
+    ap.add_argument("--ranks", default="0",
+                    help="--solo: the ranks to rehearse one after the other ('all' = 0..G-1); the node runs at its "
+                    "slowest rank, so node_estimate = the minimum over them")
+    ap.add_argument("--exchange-ns", type=int, default=0,
+                    help="--solo: charge every exchange this latency (SPX_REHEARSAL_EXCHANGE_NS; 0 = free)")
+    ap.add_argument("--exchange-list", default="",
+                    help="--solo: after the ranks, the slowest one again with every exchange charged each of these "
+                    "latencies (ns, comma-separated)")
     a = ap.parse_args()
+    if a.exchange_ns:
+        os.environ["SPX_REHEARSAL_EXCHANGE_NS"] = str(a.exchange_ns)
     os.environ.setdefault("SPX_BLOCKING_SYNC", "1")
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     os.environ.setdefault("SPX_SYNC_POLL_US", str(bench.sync_poll_for(a.G)))
     spx = bench.load_product()
     G, B, P = a.G, a.inflight or bench.inflight_for(a.G), a.proofs
     world = G
+    solo_ranks = [0]
     if a.solo:
-        G = 1  # one rank object, acting as rank 0 of `world`
+        G = 1  # one rank object, acting as each rank of --ranks in turn
+        solo_ranks = list(range(world)) if a.ranks == "all" else [int(x) for x in a.ranks.split(",")]
     groups = [spx.CommGroup(G) for _ in range(B)]
     ctxs = [[spx.Context(0) for _ in range(B)] for _ in range(G)]
     for r in range(G):
         for k in range(B):
             ctxs[r][k].set_lvl0_batch(bench.lvl0_for(world) if a.lvl0 == -2 else a.lvl0)
             if a.solo:
-                ctxs[r][k].set_comm_rehearsal(0, world)
+                ctxs[r][k].set_comm_rehearsal(solo_ranks[0], world)
             elif G > 1:
                 ctxs[r][k].set_comm_group(groups[k], r)
     n = 1 << a.log_n
@@ -91,16 +103,43 @@ def main():
         assert all(o == out[0] for o in out), "ranks disagree"
         return out[0], el, time.process_time() - c0
 
-    if a.warmup:
+    def sync_barrier():
+        if a.sync_dir:
+            os.makedirs(a.sync_dir, exist_ok=True)
+            open(os.path.join(a.sync_dir, "ready.%d" % os.getpid()), "w").close()
+            t_wait = time.time()
+            while len([f for f in os.listdir(a.sync_dir) if f.startswith("ready.")]) < a.sync_n:
+                if time.time() - t_wait > 600:
+                    raise SystemExit("side-by-side barrier timed out")
+                time.sleep(0.01)
+
+    per_rank, with_exchange = {}, {}
+    cur = {"rank": solo_ranks[0]}
+
+    def set_rank(rr, delay_ns):
+        """solo contexts act as rank rr of `world`, each exchange charged delay_ns (read when the comm is set)"""
+        os.environ["SPX_REHEARSAL_EXCHANGE_NS"] = str(delay_ns)
+        for c in ctxs[0]:
+            c.set_comm_rehearsal(rr, world)
+        if rr != cur["rank"]:  # a rank's index holds its own rows and columns
+            pks[0] = None
+            pks[0] = spx.IndexPK(ctxs[0][0], bench.index_from_c(spx, ctxs[0][0], mats), a.log_n)
+            cur["rank"] = rr
+
+    if a.solo and (len(solo_ranks) > 1 or a.exchange_list):
+        # every rank but the last: a warm-up step and the timed steps; the last is the main run below
+        for rr in solo_ranks[:-1]:
+            set_rank(rr, a.exchange_ns)
+            if a.warmup:
+                run(1)
+            _, el_r, _ = run(a.steps)
+            per_rank[rr] = round(a.steps * P * n / el_r, 1)
+        set_rank(solo_ranks[-1], a.exchange_ns)
+        if a.warmup:
+            run(1)
+    elif a.warmup:
         run(a.warmup)
-    if a.sync_dir:
-        os.makedirs(a.sync_dir, exist_ok=True)
-        open(os.path.join(a.sync_dir, "ready.%d" % os.getpid()), "w").close()
-        t_wait = time.time()
-        while len([f for f in os.listdir(a.sync_dir) if f.startswith("ready.")]) < a.sync_n:
-            if time.time() - t_wait > 600:
-                raise SystemExit("side-by-side barrier timed out")
-            time.sleep(0.01)
+    sync_barrier()
     hp0 = spx.host_phase_stats()
     proofs, el, cpu = run(a.steps)
     hp1 = spx.host_phase_stats()
@@ -108,11 +147,26 @@ def main():
     host_phases = {k: {"cpu_ms": round((hp1[k][0] - hp0[k][0]) / npf * 1e3, 3),
                        "wall_ms": round((hp1[k][1] - hp0[k][1]) / npf * 1e3, 3)} for k in hp1}
     t_end = time.time()
-    print(json.dumps({"G": world, "solo_rank0": a.solo, "t_start": round(t_end - el, 3), "t_end": round(t_end, 3), "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
+    if a.solo:
+        per_rank[solo_ranks[-1]] = round(a.steps * P * n / el, 1)
+    node = min(per_rank.values()) if per_rank else None
+    if a.solo and a.exchange_list:
+        # the slowest rank again, every exchange charged each listed latency
+        slow = min(per_rank, key=per_rank.get)
+        for d in [int(x) for x in a.exchange_list.split(",")]:
+            set_rank(slow, d)
+            run(1)
+            _, el_d, _ = run(a.steps)
+            with_exchange[str(d)] = round(a.steps * P * n / el_d, 1)
+        set_rank(slow, a.exchange_ns)
+    print(json.dumps({"G": world, "solo_rank0": a.solo, "solo_ranks": solo_ranks if a.solo else None,
+                      "per_rank": {str(k): v for k, v in sorted(per_rank.items())} if a.solo else None,
+                      "exchange_ns": a.exchange_ns, "slowest_rank_with_exchange_ns": with_exchange or None, "t_start": round(t_end - el, 3), "t_end": round(t_end, 3), "inflight_per_rank": B, "proofs": len(proofs), "log_n": a.log_n, "cached": a.cached,
                       "value": round(a.steps * P * n / el, 1), "ms_per_proof": round(el / (a.steps * P) * 1e3, 3),
-                      # strong scaling: every rank works on every proof, so the node finishes the batch when
-                      # rank 0 does (ranks are symmetric; exchanges taken as free)
-                      "node_estimate": round(a.steps * P * n / el, 1) if a.solo else None,
+                      # strong scaling: every rank works on every proof, so the node finishes the batch when its
+                      # slowest rank does (the minimum over the rehearsed ranks)
+                      "node_estimate": node,
+                      "node_spread": round(max(per_rank.values()) / node, 4) if per_rank else None,
                       "distinct": len(set(proofs)),
                       "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs), "device_memory": mem,
                       "process_cores_busy": round(cpu / el, 2),

@@ -1248,18 +1248,31 @@ __global__ __launch_bounds__(kThreads) void k_spmv_sliced_group(SpmvSlicedView v
             dst[j] = v.dst[i];
             a[j] = ld_fr(v.val + i);
         }
-        for (int p = 0; p < k; ++p) {
-            const SpmvJob& J = g.j[p];
-            Fr zv[kSpmvPer];
+        // two proofs at a time: both proofs' gathers are issued before the first product (the stores of
+        // one proof could otherwise alias the next proof's z as far as the compiler knows, which would
+        // serialise every gather behind the previous proof's stores)
+        for (int p = 0; p < k; p += 2) {
+            const bool two = p + 1 < k;
+            const SpmvJob& J0 = g.j[p];
+            const SpmvJob& J1 = g.j[two ? p + 1 : p];
+            Fr z0[kSpmvPer], z1[kSpmvPer];
 #pragma unroll
-            for (uint32_t j = 0; j < kSpmvPer; ++j) zv[j] = ld_fr(J.z + col[j]);
+            for (uint32_t j = 0; j < kSpmvPer; ++j) {
+                z0[j] = ld_fr(J0.z + col[j]);
+                z1[j] = ld_fr(J1.z + col[j]);
+            }
 #pragma unroll
             for (uint32_t j = 0; j < kSpmvPer; ++j) {
                 if (c0 + j * kThreads + threadIdx.x < r1) {
-                    Fr t;
-                    fe_mul(t, a[j], zv[j]);
                     const uint32_t m = dst[j] >> 30, x = dst[j] & 0x3FFFFFFFu;
-                    st_fr((m == 0 ? J.o[0] : (m == 1 ? J.o[1] : J.o[2])) + x, t);
+                    Fr t0, t1;
+                    if (two) {
+                        fr_mul_pair(t0, a[j], z0[j], t1, a[j], z1[j]);
+                        st_fr((m == 0 ? J1.o[0] : (m == 1 ? J1.o[1] : J1.o[2])) + x, t1);
+                    } else {
+                        fe_mul(t0, a[j], z0[j]);
+                    }
+                    st_fr((m == 0 ? J0.o[0] : (m == 1 ? J0.o[1] : J0.o[2])) + x, t0);
                 }
             }
         }

@@ -92,6 +92,13 @@ int spx_comm_hub_create_rccl(const uint8_t id[128], int rank, int world, int dev
  * context), and over the in-process test group (virtual ranks as host threads; spx_comm_group_create) */
 int spx_comm_hub_create_shm(const char *name, int rank, int world, void **hub_out);
 int spx_comm_hub_create_group(void *group, int rank, void **hub_out);
+/* ... and over a caller-provided collective (e.g. a torch.distributed process group: gloo on the CPU,
+ * RCCL = backend "nccl" on MI355X): fn(user, send, recv, bytes) must gather `bytes` from every rank of
+ * the caller's group into recv in rank order and return 0 (non-zero fails the exchange with
+ * SPX_DEVICE); rank / world are the caller's group's. Only the hub's thread calls fn, in the same
+ * sequence on every rank. */
+typedef int (*spx_allgather_fn)(void *user, const void *send, void *recv, size_t bytes);
+int spx_comm_hub_create_callback(spx_allgather_fn fn, void *user, int rank, int world, void **hub_out);
 int spx_ctx_set_comm_hub(spx_ctx *ctx, void *hub, int channel);
 /* one exchange on `channel` without a context (transport tests); blocks until every rank posted it */
 int spx_comm_hub_allgather(void *hub, int channel, const void *send, void *recv, size_t bytes);
@@ -275,7 +282,7 @@ enum {
     SPX_K_MTV = 3,      /* sum_m r_m M(r_x, .) */
     SPX_K_OPEN = 4,     /* mKZG quotient / fold level */
     SPX_K_EQ = 5,       /* eq tables */
-    SPX_K_MSM_SORT = 6, /* digit count + scatter (both curves) */
+    SPX_K_MSM_SORT = 6, /* the bucket sort: k_sort_count .. k_sort_final (both curves) */
     SPX_K_ACC_G1 = 7,   /* bucket accumulation, affine level, G1 */
     SPX_K_ACC_G2 = 8,   /* bucket accumulation, affine level, G2 */
     SPX_K_ACCX_G1 = 9,  /* bucket accumulation, XYZZ levels, G1 */

@@ -87,6 +87,7 @@ EXPORTED = [
     "spx_comm_hub_create_rccl",
     "spx_comm_hub_create_shm",
     "spx_comm_hub_create_group",
+    "spx_comm_hub_create_callback",
     "spx_ctx_set_comm_hub",
     "spx_comm_hub_allgather",
     "spx_comm_hub_stats",
@@ -185,6 +186,8 @@ def lib():
         L.spx_comm_hub_create_rccl.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.spx_comm_hub_create_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.spx_comm_hub_create_group.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+        if hasattr(L, "spx_comm_hub_create_callback") or not os.environ.get("SPX_LIB_PATH"):
+            L.spx_comm_hub_create_callback.argtypes = [ALLGATHER_FN, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.spx_ctx_set_comm_hub.argtypes = [vp, vp, ctypes.c_int]
         L.spx_comm_hub_allgather.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p, sz]
         L.spx_comm_hub_stats.argtypes = [vp, ctypes.c_void_p]
@@ -421,10 +424,15 @@ class ShmComm:
             pass
 
 
+# spx_allgather_fn: (user, send, recv, bytes) -> 0 on success
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
 class ExchangeHub:
     """One collective transport per rank shared by every proof in flight, ordered by channel
-    (comm_hub.cpp): ExchangeHub.rccl(uid, rank, world, device), .shm(name, rank, world) or
-    .group(CommGroup, rank)."""
+    (comm_hub.cpp): ExchangeHub.rccl(uid, rank, world, device), .shm(name, rank, world),
+    .group(CommGroup, rank) or .torch_group(process_group) (a torch.distributed group: gloo on the CPU,
+    RCCL as backend "nccl")."""
 
     def __init__(self, h, world):
         self.h, self.world = h, int(world)
@@ -446,6 +454,36 @@ class ExchangeHub:
         h = ctypes.c_void_p()
         _check(lib().spx_comm_hub_create_group(group.h, int(rank), ctypes.byref(h)))
         return cls(h, group.world)
+
+    @classmethod
+    def torch_group(cls, group=None):
+        """the hub over a torch.distributed process group (spx_comm_hub_create_callback): the hub's thread
+        calls dist.all_gather on uint8 tensors (CPU tensors for gloo, the current device's otherwise)"""
+        import torch
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        dev = "cpu" if dist.get_backend(group) == "gloo" else "cuda:%d" % torch.cuda.current_device()
+
+        def fn(_user, send, recv, nbytes):
+            try:
+                if nbytes == 0:
+                    return 0
+                t = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8).to(dev)
+                outs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+                dist.all_gather(outs, t, group=group)
+                buf = torch.cat(outs).cpu().numpy().tobytes()
+                ctypes.memmove(recv, buf, len(buf))
+                return 0
+            except Exception:  # reported to the waiting exchange as SPX_DEVICE
+                return 1
+
+        cb = ALLGATHER_FN(fn)
+        h = ctypes.c_void_p()
+        _check(lib().spx_comm_hub_create_callback(cb, None, rank, world, ctypes.byref(h)))
+        hub = cls(h, world)
+        hub._cb = cb  # the C side holds the function pointer: keep the thunk alive with the hub
+        return hub
 
     def allgather(self, channel, data):
         data = bytes(data)

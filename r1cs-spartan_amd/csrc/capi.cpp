@@ -200,6 +200,29 @@ int spx_comm_hub_create_shm(const char* name, int rank, int world, void** hub_ou
         *hub_out = new std::shared_ptr<spx::OrderedHub>(spx::make_hub(spx::make_shm_comm(name, rank, world)));
     });
 }
+namespace spx {
+// a caller-provided allgather (spx_comm_hub_create_callback)
+struct CallbackComm : Comm {
+    spx_allgather_fn fn;
+    void* user;
+    int r, w;
+    CallbackComm(spx_allgather_fn f, void* u, int rank, int world) : fn(f), user(u), r(rank), w(world) {}
+    int rank() const override { return r; }
+    int size() const override { return w; }
+    void allgather(const void* s, void* rv, size_t b) override {
+        const int rc = fn(user, s, rv, b);
+        if (rc != 0) throw SpxError(kDevice, "caller-provided allgather failed (" + std::to_string(rc) + ")");
+    }
+};
+}  // namespace spx
+int spx_comm_hub_create_callback(spx_allgather_fn fn, void* user, int rank, int world, void** hub_out) {
+    return guard([&] {
+        if (!hub_out || !fn) spx::invalid("null argument");
+        if (world < 1 || rank < 0 || rank >= world) spx::invalid("bad rank / world");
+        *hub_out = new std::shared_ptr<spx::OrderedHub>(
+            spx::make_hub(std::unique_ptr<spx::Comm>(new spx::CallbackComm(fn, user, rank, world))));
+    });
+}
 int spx_comm_hub_create_group(void* group, int rank, void** hub_out) {
     return guard([&] {
         if (!hub_out || !group) spx::invalid("null argument");

@@ -56,7 +56,10 @@ CLOCK_FILE = os.path.join(ROOT, "profiles", "r05", "r05a_clock.json")
 # long for every bench run: tools/cpu_baseline_1core.py, run once, proof byte-equal to the GPU's)
 CPU1_2_20_FILE = os.path.join(ROOT, "profiles", "r05", "r05a_cpu_baseline_1core_2_20.json")
 # BASELINE C5 (2^24, 8 ranks) byte parity and the oracle's 16-core time there (tools/c5_parity.py)
-C5_FILE = os.path.join(ROOT, "profiles", "r05", "r05d_c5_parity_2_24.json")
+# the newest committed 2^24 8-rank byte-parity record (tools/c5_parity.py --commit REV)
+C5_FILE = next((f for f in (os.path.join(ROOT, "profiles", "r06", "r06_c5_parity_2_24.json"),
+                            os.path.join(ROOT, "profiles", "r05", "r05d_c5_parity_2_24.json")) if os.path.exists(f)),
+               os.path.join(ROOT, "profiles", "r05", "r05d_c5_parity_2_24.json"))
 MADD_FILE = os.path.join(ROOT, "profiles", "r02_ubench_madd.txt")
 
 # HIP kernel (short rocprofv3 name) behind each kernel-stats id
@@ -1100,6 +1103,9 @@ def main():
             out["c5_parity_2_24"] = {"equal": c5.get("equal"), "ranks": c5.get("ranks"), "proof_bytes": c5.get("proof_bytes"),
                                      "oracle_cores": c5.get("oracle_threads"), "oracle_s": c5.get("oracle_s"),
                                      "oracle_constraints_per_s": round((1 << 24) / c5["oracle_s"], 1) if c5.get("oracle_s") else None,
+                                     # the revision the record pins (round 5's record predates the field:
+                                     # it was made at 239b49d)
+                                     "commit": c5.get("commit") or "239b49d",
                                      "source": c5["source"]}
         out["host"] = {"cpu_count": os.cpu_count(), "cores_used": host_cores(),
                        "hashing_lanes": hs1[2],

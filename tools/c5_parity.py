@@ -26,10 +26,11 @@ def main():
     ap.add_argument("--log-v", type=int, default=5)
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--commit", default="", help="the git revision of the tree being pinned (recorded; the GPU box has no .git)")
     a = ap.parse_args()
     log_n, log_v, G = a.log_n, a.log_v, a.ranks
     rec = {"log_n": log_n, "log_v": log_v, "generator": "uniform-3n (kind 0), seed 0x5EED0000 + log_n", "ranks": G,
-           "pp": "GPU keygen, seed 0xC0FFEE", "t": {}}
+           "pp": "GPU keygen, seed 0xC0FFEE", "t": {}, "commit": a.commit or None}
     t0 = time.perf_counter()
 
     def mark(k):

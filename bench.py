@@ -480,6 +480,12 @@ def fit_inflight(ctxs, probe, reserve=FIT_RESERVE):
                  "reserve_GiB": round(reserve / 2**30, 2), "contexts": fit, "wanted": len(ctxs)}
 
 
+def pair_us_for(g):
+    """MSM batches merged across two contexts' proofs (spx_ctx_set_msm_pairing): the wait for a partner
+    in us, 0 = off (measured per sharding degree: DESIGN.md §6)"""
+    return 0
+
+
 def lvl0_for(g):
     """level-0 opening MSM inside the first opening's batch (one MSM pipeline less per proof) for proofs
     sharded over g >= 4 ranks, where a rank's small MSMs are latency-bound; beside the commitment otherwise"""

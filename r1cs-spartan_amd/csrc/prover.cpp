@@ -107,6 +107,8 @@ Ctx::~Ctx() {
     (void)hipSetDevice(device);
     if (msm_side) msm_ws_destroy(msm_side);
     if (side_ev) (void)hipEventDestroy(side_ev);
+    if (pair_ready) (void)hipEventDestroy(pair_ready);
+    if (pair_done) (void)hipEventDestroy(pair_done);
     if (side) (void)hipStreamDestroy(side);
     msm_ws_destroy(msm);
     scratch.release();
@@ -906,6 +908,117 @@ static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
     return all;
 }
 
+// ---------------------------------------------------------------- MSM batches of two proofs merged
+// (spx_ctx_set_msm_pairing). A rank of a G-rank proof runs 1/G of each MSM: its accumulation grids
+// are one round of resident waves deep and every batch pays its own latency-bound tail (partial
+// levels, weighting tree, the sort's launches). When another context of this process reaches the
+// same batch of its own proof (same curve, kind, shape, public parameter and shard), the two batches
+// run as ONE on the context that arrives second: its stream waits for the first one's scalars (an
+// event), the merged instance list runs through the MSM pipeline once (grids twice as deep, one tail
+// for both), and each proof's outputs and the shared status words are copied into its own output
+// buffer, after which the first context's stream continues (an event recorded by the second). Every
+// instance keeps its own scalars (MsmInst::sc) and its owner rank (MsmInst::own1), so every output
+// is the one an unmerged batch gives; an overflowed merged batch makes both proofs rerun theirs
+// dense, alone. A context that finds no partner within pair_us microseconds runs its batch alone.
+struct PairPost {
+    bool g2;
+    int kind, ninst, rank, world;
+    uint32_t size0;
+    const void* pts;
+    Ctx* C;
+    std::vector<MsmInst> insts;  // sc and own1 set
+    void* out;
+    hipEvent_t ready, done;
+    bool taken = false, finished = false;
+    std::exception_ptr err;
+    bool matches(const PairPost& o) const {
+        return g2 == o.g2 && kind == o.kind && ninst == o.ninst && rank == o.rank && world == o.world &&
+               size0 == o.size0 && pts == o.pts && C != o.C;
+    }
+};
+static std::mutex g_pair_mu;
+static std::condition_variable g_pair_cv;
+static std::vector<PairPost*> g_pair_wait;
+enum { kPairCommit = 1, kPairLvl0, kPairOpen };
+
+static void msm_run_any(Ctx& C, bool g2, const MsmInst* insts, int n, const void* pts, const Fr* scalars, void* out,
+                        const MsmShard& sh) {
+    if (g2)
+        msm_run_g2(C.msm, insts, n, static_cast<const G2Aff*>(pts), scalars, out, C.stream, sh);
+    else
+        msm_run_g1(C.msm, insts, n, static_cast<const G1Slot*>(pts), scalars, out, C.stream, sh);
+}
+static void msm_batch(Ctx& C, bool g2, int kind, const MsmInst* insts, int n, const void* pts, const Fr* scalars, void* out,
+                      const MsmShard& sh) {
+    const int us = C.pair_us.load(std::memory_order_relaxed);
+    if (us <= 0 || sh.dense || n <= 0) {
+        msm_run_any(C, g2, insts, n, pts, scalars, out, sh);
+        return;
+    }
+    PairPost me;
+    me.g2 = g2, me.kind = kind, me.ninst = n, me.rank = sh.rank, me.world = sh.world;
+    me.size0 = insts[0].size, me.pts = pts, me.C = &C, me.out = out;
+    me.insts.assign(insts, insts + n);
+    for (int i = 0; i < n; ++i) {
+        if (!me.insts[i].sc) me.insts[i].sc = scalars + me.insts[i].scalar_off;
+        me.insts[i].own1 = (uint32_t)i + 1;
+    }
+    C.ensure_pair_events();
+    me.ready = C.pair_ready, me.done = C.pair_done;
+    SPX_HIP(hipEventRecord(me.ready, C.stream));
+    PairPost* first = nullptr;
+    {
+        std::unique_lock<std::mutex> lk(g_pair_mu);
+        for (auto it = g_pair_wait.begin(); it != g_pair_wait.end(); ++it)
+            if ((*it)->matches(me)) {
+                first = *it;
+                g_pair_wait.erase(it);
+                first->taken = true;
+                break;
+            }
+        if (!first) {  // wait for a partner to take this batch
+            g_pair_wait.push_back(&me);
+            if (!g_pair_cv.wait_for(lk, std::chrono::microseconds(us), [&] { return me.taken; })) {
+                g_pair_wait.erase(std::find(g_pair_wait.begin(), g_pair_wait.end(), &me));
+                lk.unlock();
+                ++C.msm_alone;
+                msm_run_any(C, g2, me.insts.data(), n, pts, nullptr, out, sh);
+                return;
+            }
+            g_pair_cv.wait(lk, [&] { return me.finished; });
+            if (me.err) std::rethrow_exception(me.err);
+            lk.unlock();
+            SPX_HIP(hipStreamWaitEvent(C.stream, me.done, 0));  // the merged batch has filled `out`
+            return;
+        }
+    }
+    // second to arrive: the merged batch on this context's stream and MSM workspace
+    try {
+        SPX_HIP(hipStreamWaitEvent(C.stream, first->ready, 0));
+        std::vector<MsmInst> all(me.insts);
+        all.insert(all.end(), first->insts.begin(), first->insts.end());
+        const size_t psz = g2 ? 4 * 96 : 4 * 48;
+        uint8_t* mo = C.buf<uint8_t>(Ctx::kSlotPairOut, msm_out_bytes(g2, 2 * n));
+        msm_run_any(C, g2, all.data(), 2 * n, pts, nullptr, mo, sh);
+        const size_t rb = psz * n;
+        SPX_HIP(hipMemcpyAsync(out, mo, rb, hipMemcpyDeviceToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync((uint8_t*)out + rb, mo + 2 * rb, 16, hipMemcpyDeviceToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(first->out, mo + rb, rb, hipMemcpyDeviceToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync((uint8_t*)first->out + rb, mo + 2 * rb, 16, hipMemcpyDeviceToDevice, C.stream));
+        SPX_HIP(hipEventRecord(first->done, C.stream));
+        ++C.msm_merged;
+    } catch (...) {
+        std::lock_guard<std::mutex> lk(g_pair_mu);
+        first->err = std::current_exception();
+        first->finished = true;
+        g_pair_cv.notify_all();
+        throw;
+    }
+    std::lock_guard<std::mutex> lk(g_pair_mu);
+    first->finished = true;
+    g_pair_cv.notify_all();
+}
+
 // ---------------------------------------------------------------- commit (commit.rs:17-29)
 // Split in two so the MSM runs while the host absorbs the matrices into the transcript: launch
 // enqueues the MSM and the copy of its XYZZ result into pinned memory; finish waits and decodes.
@@ -920,7 +1033,7 @@ static void commit_launch(Ctx& C, PP& P, const Fr* z, uint64_t n, const MsmShard
     inst.W = (uint32_t)P.g1_W;
     const size_t ob = msm_out_bytes(false, 1);
     void* out = C.buf(Ctx::kSlotCommit, ob);
-    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, C.stream, sh);
+    msm_batch(C, false, kPairCommit, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, sh);
     SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, C.stream));
 }
 static Affine<HFq> commit_finish(Ctx& C, PP& P, const Fr* z, uint64_t n, Comm& comm) {
@@ -970,7 +1083,10 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z, int L, const MsmShard& sh, b
     I.W = (uint32_t)P.g2_W[0];
     const size_t ob = msm_out_bytes(true, 1);
     void* out = C.buf(Ctx::kSlotLvl0Out, ob);
-    msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
+    if (on_side)
+        msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
+    else
+        msm_batch(C, true, kPairLvl0, &I, 1, P.g2_pre.as<G2Aff>(), q, out, sh);
     SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
 }
 static Affine<HFq2> lvl0_finish(Ctx& C, PP& P, const Fr* z, int L, Comm& comm, bool on_side = false) {
@@ -1068,7 +1184,7 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
         MsmShard sh = shard_of(comm);
         sh.dense = attempt > 0;
         if (nm) {
-            msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream, sh);
+            msm_batch(C, true, kPairOpen, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, sh);
             SPX_HIP(hipMemcpyAsync(h, out, ob, hipMemcpyDeviceToHost, C.stream));
         }
         if (!attempt) SPX_HIP(hipMemcpyAsync(h + ob, rin, 32, hipMemcpyDeviceToHost, C.stream));

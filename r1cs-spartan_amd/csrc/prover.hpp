@@ -195,7 +195,7 @@ struct Ctx {
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
-    enum { kSlotCommit, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
+    enum { kSlotCommit, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlotPairOut, kSlots };
     DevMem slot[kSlots];
     template <class T = void>
     T* buf(int id, size_t bytes) {
@@ -227,6 +227,16 @@ struct Ctx {
     // spx_prove_many on this context proves its stubbed-commitment, unsharded proofs in lockstep groups
     // of this many (prove_group; 1 = one at a time)
     std::atomic<int> group{1};
+    // MSM batches merged with another context's identical batch (prover.cpp msm_batch): wait up to
+    // this many microseconds for a partner (0 = never merge); the batches merged (as the second
+    // context) and run alone after waiting
+    std::atomic<int> pair_us{0};
+    std::atomic<uint64_t> msm_merged{0}, msm_alone{0};
+    hipEvent_t pair_ready = nullptr, pair_done = nullptr;
+    void ensure_pair_events() {
+        if (!pair_ready) SPX_HIP(hipEventCreateWithFlags(&pair_ready, hipEventDisableTiming));
+        if (!pair_done) SPX_HIP(hipEventCreateWithFlags(&pair_done, hipEventDisableTiming));
+    }
     void wait_stream(hipStream_t s);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
         wait_stream(stream);

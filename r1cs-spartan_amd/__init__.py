@@ -370,10 +370,14 @@ class Context:
     def set_msm_pairing(self, us):
         """merge this context's MSM batches with other contexts' identical batches, waiting up to `us`
         microseconds for a partner (0 = never; spx_ctx_set_msm_pairing)"""
+        if not hasattr(lib(), "spx_ctx_set_msm_pairing") and not us:  # an A/B build that predates it
+            return
         _check(lib().spx_ctx_set_msm_pairing(self.h, int(us)))
 
     def msm_pairing_stats(self):
         """(batches merged as the second context, batches run alone after waiting)"""
+        if not hasattr(lib(), "spx_ctx_msm_pairing_stats"):
+            return 0, 0
         out = (ctypes.c_uint64 * 2)()
         _check(lib().spx_ctx_msm_pairing_stats(self.h, out))
         return out[0], out[1]

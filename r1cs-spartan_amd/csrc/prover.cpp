@@ -913,13 +913,16 @@ static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
 // are one round of resident waves deep and every batch pays its own latency-bound tail (partial
 // levels, weighting tree, the sort's launches). When another context of this process reaches the
 // same batch of its own proof (same curve, kind, shape, public parameter and shard), the two batches
-// run as ONE on the context that arrives second: its stream waits for the first one's scalars (an
-// event), the merged instance list runs through the MSM pipeline once (grids twice as deep, one tail
-// for both), and each proof's outputs and the shared status words are copied into its own output
-// buffer, after which the first context's stream continues (an event recorded by the second). Every
-// instance keeps its own scalars (MsmInst::sc) and its owner rank (MsmInst::own1), so every output
-// is the one an unmerged batch gives; an overflowed merged batch makes both proofs rerun theirs
-// dense, alone. A context that finds no partner within pair_us microseconds runs its batch alone.
+// run as ONE on the context that arrives second: it waits on the host until the first one's scalars
+// are in place (an event), runs the merged instance list through the MSM pipeline once (grids twice
+// as deep, one tail for both) and copies each proof's outputs and the shared status words straight
+// into that proof's pinned host buffer; the first context's next sync also waits for the event the
+// second records after those copies. No stream ever waits on another stream's event: with more
+// streams than hardware queues such a wait blocks the queue for every stream mapped to it (measured:
+// a G = 8 rank fell from 418 to 240 M constraints/s with stream-side waits). Every instance keeps its
+// own scalars (MsmInst::sc) and its owner rank (MsmInst::own1), so every output is the one an
+// unmerged batch gives; an overflowed merged batch makes both proofs rerun theirs dense, alone. A
+// context that finds no partner within pair_us microseconds runs its batch alone.
 struct PairPost {
     bool g2;
     int kind, ninst, rank, world;
@@ -927,7 +930,7 @@ struct PairPost {
     const void* pts;
     Ctx* C;
     std::vector<MsmInst> insts;  // sc and own1 set
-    void* out;
+    uint8_t* host;               // pinned destination of the outputs + status words
     hipEvent_t ready, done;
     bool taken = false, finished = false;
     std::exception_ptr err;
@@ -948,16 +951,24 @@ static void msm_run_any(Ctx& C, bool g2, const MsmInst* insts, int n, const void
     else
         msm_run_g1(C.msm, insts, n, static_cast<const G1Slot*>(pts), scalars, out, C.stream, sh);
 }
+// One MSM batch of this proof on C.stream: outputs (msm_out_bytes) in `out` and copied to the pinned
+// `host` (ready after this context's next sync), merged with another context's identical batch when
+// possible (above).
 static void msm_batch(Ctx& C, bool g2, int kind, const MsmInst* insts, int n, const void* pts, const Fr* scalars, void* out,
-                      const MsmShard& sh) {
+                      uint8_t* host, const MsmShard& sh) {
+    const size_t ob = msm_out_bytes(g2, n);
     const int us = C.pair_us.load(std::memory_order_relaxed);
+    auto alone = [&](const MsmInst* in, const Fr* sc) {
+        msm_run_any(C, g2, in, n, pts, sc, out, sh);
+        SPX_HIP(hipMemcpyAsync(host, out, ob, hipMemcpyDeviceToHost, C.stream));
+    };
     if (us <= 0 || sh.dense || n <= 0) {
-        msm_run_any(C, g2, insts, n, pts, scalars, out, sh);
+        alone(insts, scalars);
         return;
     }
     PairPost me;
     me.g2 = g2, me.kind = kind, me.ninst = n, me.rank = sh.rank, me.world = sh.world;
-    me.size0 = insts[0].size, me.pts = pts, me.C = &C, me.out = out;
+    me.size0 = insts[0].size, me.pts = pts, me.C = &C, me.host = host;
     me.insts.assign(insts, insts + n);
     for (int i = 0; i < n; ++i) {
         if (!me.insts[i].sc) me.insts[i].sc = scalars + me.insts[i].scalar_off;
@@ -982,29 +993,27 @@ static void msm_batch(Ctx& C, bool g2, int kind, const MsmInst* insts, int n, co
                 g_pair_wait.erase(std::find(g_pair_wait.begin(), g_pair_wait.end(), &me));
                 lk.unlock();
                 ++C.msm_alone;
-                msm_run_any(C, g2, me.insts.data(), n, pts, nullptr, out, sh);
+                alone(me.insts.data(), nullptr);
                 return;
             }
             g_pair_cv.wait(lk, [&] { return me.finished; });
             if (me.err) std::rethrow_exception(me.err);
-            lk.unlock();
-            SPX_HIP(hipStreamWaitEvent(C.stream, me.done, 0));  // the merged batch has filled `out`
+            C.pair_pending = me.done;  // this context's next sync waits for the merged batch's copies
             return;
         }
     }
     // second to arrive: the merged batch on this context's stream and MSM workspace
     try {
-        SPX_HIP(hipStreamWaitEvent(C.stream, first->ready, 0));
+        SPX_HIP(hipEventSynchronize(first->ready));  // the first proof's scalars are in place
         std::vector<MsmInst> all(me.insts);
         all.insert(all.end(), first->insts.begin(), first->insts.end());
-        const size_t psz = g2 ? 4 * 96 : 4 * 48;
+        const size_t rb = (g2 ? 4 * 96 : 4 * 48) * (size_t)n;
         uint8_t* mo = C.buf<uint8_t>(Ctx::kSlotPairOut, msm_out_bytes(g2, 2 * n));
         msm_run_any(C, g2, all.data(), 2 * n, pts, nullptr, mo, sh);
-        const size_t rb = psz * n;
-        SPX_HIP(hipMemcpyAsync(out, mo, rb, hipMemcpyDeviceToDevice, C.stream));
-        SPX_HIP(hipMemcpyAsync((uint8_t*)out + rb, mo + 2 * rb, 16, hipMemcpyDeviceToDevice, C.stream));
-        SPX_HIP(hipMemcpyAsync(first->out, mo + rb, rb, hipMemcpyDeviceToDevice, C.stream));
-        SPX_HIP(hipMemcpyAsync((uint8_t*)first->out + rb, mo + 2 * rb, 16, hipMemcpyDeviceToDevice, C.stream));
+        SPX_HIP(hipMemcpyAsync(host, mo, rb, hipMemcpyDeviceToHost, C.stream));
+        SPX_HIP(hipMemcpyAsync(host + rb, mo + 2 * rb, 16, hipMemcpyDeviceToHost, C.stream));
+        SPX_HIP(hipMemcpyAsync(first->host, mo + rb, rb, hipMemcpyDeviceToHost, C.stream));
+        SPX_HIP(hipMemcpyAsync(first->host + rb, mo + 2 * rb, 16, hipMemcpyDeviceToHost, C.stream));
         SPX_HIP(hipEventRecord(first->done, C.stream));
         ++C.msm_merged;
     } catch (...) {
@@ -1033,8 +1042,7 @@ static void commit_launch(Ctx& C, PP& P, const Fr* z, uint64_t n, const MsmShard
     inst.W = (uint32_t)P.g1_W;
     const size_t ob = msm_out_bytes(false, 1);
     void* out = C.buf(Ctx::kSlotCommit, ob);
-    msm_batch(C, false, kPairCommit, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, sh);
-    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, C.stream));
+    msm_batch(C, false, kPairCommit, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, C.pin_at(Ctx::kPinCommit, ob, 4 << 10), sh);
 }
 static Affine<HFq> commit_finish(Ctx& C, PP& P, const Fr* z, uint64_t n, Comm& comm) {
     C.sync();
@@ -1083,11 +1091,12 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z, int L, const MsmShard& sh, b
     I.W = (uint32_t)P.g2_W[0];
     const size_t ob = msm_out_bytes(true, 1);
     void* out = C.buf(Ctx::kSlotLvl0Out, ob);
-    if (on_side)
+    if (on_side) {
         msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
-    else
-        msm_batch(C, true, kPairLvl0, &I, 1, P.g2_pre.as<G2Aff>(), q, out, sh);
-    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
+        SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
+    } else {
+        msm_batch(C, true, kPairLvl0, &I, 1, P.g2_pre.as<G2Aff>(), q, out, C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), sh);
+    }
 }
 static Affine<HFq2> lvl0_finish(Ctx& C, PP& P, const Fr* z, int L, Comm& comm, bool on_side = false) {
     if (on_side)
@@ -1184,8 +1193,7 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
         MsmShard sh = shard_of(comm);
         sh.dense = attempt > 0;
         if (nm) {
-            msm_batch(C, true, kPairOpen, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, sh);
-            SPX_HIP(hipMemcpyAsync(h, out, ob, hipMemcpyDeviceToHost, C.stream));
+            msm_batch(C, true, kPairOpen, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, h, sh);
         }
         if (!attempt) SPX_HIP(hipMemcpyAsync(h + ob, rin, 32, hipMemcpyDeviceToHost, C.stream));
         C.sync();
@@ -1288,6 +1296,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             if (std::uncaught_exceptions() <= pending) return;
             (void)hipStreamSynchronize(C.stream);
             if (C.side) (void)hipStreamSynchronize(C.side);
+            if (C.pair_pending) {  // a merged MSM batch may still read this proof's scalars
+                (void)hipEventSynchronize(C.pair_pending);
+                C.pair_pending = nullptr;
+            }
             msm_ws_staging_reset(C.msm);
             if (C.msm_side) msm_ws_staging_reset(C.msm_side);
         }

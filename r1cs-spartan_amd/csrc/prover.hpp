@@ -233,6 +233,9 @@ struct Ctx {
     std::atomic<int> pair_us{0};
     std::atomic<uint64_t> msm_merged{0}, msm_alone{0};
     hipEvent_t pair_ready = nullptr, pair_done = nullptr;
+    // set when this context's last MSM batch ran merged on another context: the event recorded there
+    // after this proof's outputs reached its pinned buffer (sync() waits for it)
+    hipEvent_t pair_pending = nullptr;
     void ensure_pair_events() {
         if (!pair_ready) SPX_HIP(hipEventCreateWithFlags(&pair_ready, hipEventDisableTiming));
         if (!pair_done) SPX_HIP(hipEventCreateWithFlags(&pair_done, hipEventDisableTiming));
@@ -240,6 +243,10 @@ struct Ctx {
     void wait_stream(hipStream_t s);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
         wait_stream(stream);
+        if (pair_pending) {  // and a merged MSM batch that carried this proof's instances
+            SPX_HIP(hipEventSynchronize(pair_pending));
+            pair_pending = nullptr;
+        }
         msm_ws_staging_reset(msm);
         if (kprof.on) kprof.harvest();
     }

@@ -480,12 +480,6 @@ def fit_inflight(ctxs, probe, reserve=FIT_RESERVE):
                  "reserve_GiB": round(reserve / 2**30, 2), "contexts": fit, "wanted": len(ctxs)}
 
 
-def pair_us_for(g):
-    """MSM batches merged across two contexts' proofs (spx_ctx_set_msm_pairing): the wait for a partner
-    in us, 0 = off (measured per sharding degree: DESIGN.md §6)"""
-    return 0
-
-
 def lvl0_for(g):
     """level-0 opening MSM inside the first opening's batch (one MSM pipeline less per proof) for proofs
     sharded over g >= 4 ranks, where a rank's small MSMs are latency-bound; beside the commitment otherwise"""
@@ -643,8 +637,7 @@ def run_rehearsal(args, log_n, log_v, P):
         cmd = [sys.executable, os.path.join(ROOT, "tools", "vrank_bench.py"), "--G", str(G), "--solo", "--ranks", "all",
                "--log-n", str(log_n), "--log-v", str(log_v), "--proofs", str(P),
                "--steps", str(min(args.steps, args.rehearse_steps)),
-               "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else []) + \
-              (["--pair-us", str(args.pair_us)] if args.pair_us >= 0 else [])
+               "--warmup", "1"] + (["--inflight", str(args.inflight)] if args.inflight else [])
         if G == gmax and lat:
             meas = max(lat["allgather_96B_us"], lat["allgather_384B_us"])
             cmd += ["--exchange-list", "%d,%d" % (max(1, int(meas * 1e3)), REHEARSAL_PESSIMISTIC_NS)]
@@ -717,9 +710,6 @@ def main():
                     "over its group's K GPUs); '' to skip")
     ap.add_argument("--rehearse", default="2,4,8",
                     help="N = 1: world sizes G for the one-rank rehearsal of a G-GPU proof-sharded node ('' to skip)")
-    ap.add_argument("--pair-us", type=int, default=-1,
-                    help="merge MSM batches of two contexts' proofs, waiting up to this many us for a partner "
-                    "(spx_ctx_set_msm_pairing; 0 = off; default: pair_us_for(world))")
     ap.add_argument("--rehearse-steps", type=int, default=10,
                     help="steps of P proofs timed per rehearsed rank (at most --steps)")
     ap.add_argument("--comm", default="shm", choices=["shm", "rccl"],
@@ -803,7 +793,6 @@ def main():
         cs = [spx.Context(device) for _ in range(k)]
         for c in cs:
             c.set_lvl0_batch(lvl0_for(world))
-            c.set_msm_pairing(pair_us_for(world) if args.pair_us < 0 else args.pair_us)
         return cs, attach(cs, args.comm)
 
     if not need_batch:
@@ -812,8 +801,6 @@ def main():
         ctxs = c2_contexts(spx, device, Bb * C2_GROUP)
     else:
         ctxs = [spx.Context(device) for _ in range(Bb)]
-        for c in ctxs:
-            c.set_msm_pairing(pair_us_for(1) if args.pair_us < 0 else args.pair_us)
     sctxs, hub = make_sharded(Bs) if need_sharded else ([], None)
     ctx = (ctxs or sctxs)[0]
     # the world size each rank's product communicator spans (one allgather of the rank ids on it)
@@ -863,13 +850,9 @@ def main():
 
     def single_fn(c, k, cached=False):
         def run():
-            c.set_msm_pairing(0)  # one proof alone: nobody to merge with, so no waiting for a partner
-            try:
-                for _ in range(args.steps):
-                    r = spx.MLArgumentForR1CS.prove_witness(k, wits[0], pp, mode=args.mode, seed=7, cached=cached,
-                                                            commitment_stub=stub)
-            finally:
-                c.set_msm_pairing(pair_us_for(world if c in sctxs else 1) if args.pair_us < 0 else args.pair_us)
+            for _ in range(args.steps):
+                r = spx.MLArgumentForR1CS.prove_witness(k, wits[0], pp, mode=args.mode, seed=7, cached=cached,
+                                                        commitment_stub=stub)
             return r
         return run
 

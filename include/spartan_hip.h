@@ -140,16 +140,6 @@ int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t by
  * with matrices absorbed per proof, sharded ranks), 0 = hipStreamSynchronize, -1 = the process default
  * (SPX_SYNC_POLL_US, else 0). */
 int spx_ctx_set_sync_poll(spx_ctx *ctx, int us);
-/* Merge this context's MSM batches with identical batches of other contexts' proofs in the same
- * process (same curve, kind, shape, public parameter and shard): the context that arrives second runs
- * both as one batch on its stream (deeper accumulation grids, one tail for both) and each proof gets
- * exactly its own outputs. A context waits up to `us` microseconds for a partner (0 = never merge,
- * the default). For throughput with many proofs in flight (a rank of a proof-sharded prove); a lone
- * proof only waits. stats: out[0] batches this context ran merged (as the second), out[1] batches it
- * ran alone after waiting. Replaces nothing in the reference (its MSMs run one at a time,
- * commit.rs:25, open.rs:49). */
-int spx_ctx_set_msm_pairing(spx_ctx *ctx, int us);
-int spx_ctx_msm_pairing_stats(spx_ctx *ctx, uint64_t out[2]);
 /* Lockstep groups for spx_prove_many (no effect on the proof bytes): with k > 1 (at most 8) the
  * context's stubbed-commitment proofs on an unsharded context (BASELINE C2) run k at a time in
  * lockstep: each sumcheck round of the k proofs is one launch (blockIdx.y = proof) with one host wait,

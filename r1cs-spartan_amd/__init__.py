@@ -97,8 +97,6 @@ EXPORTED = [
     "spx_ctx_mem_info",
     "spx_ctx_set_sync_poll",
     "spx_ctx_set_group",
-    "spx_ctx_set_msm_pairing",
-    "spx_ctx_msm_pairing_stats",
     "spx_host_phase_stats",
     "spx_pp_load",
     "spx_pp_generate",
@@ -180,9 +178,6 @@ def lib():
         L.spx_ctx_set_sync_poll.argtypes = [vp, ctypes.c_int]
     if hasattr(L, "spx_ctx_set_group") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_ctx_set_group.argtypes = [vp, ctypes.c_int]
-    if hasattr(L, "spx_ctx_set_msm_pairing") or not os.environ.get("SPX_LIB_PATH"):
-        L.spx_ctx_set_msm_pairing.argtypes = [vp, ctypes.c_int]
-        L.spx_ctx_msm_pairing_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_mem_info") or not os.environ.get("SPX_LIB_PATH"):
         L.spx_ctx_mem_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(L, "spx_ctx_set_lvl0_batch"):  # A/B builds may predate it
@@ -366,21 +361,6 @@ class Context:
         """spx_prove_many runs this context's stubbed-commitment proofs k at a time in lockstep (one launch
         per sumcheck round for the k proofs; 1 = one at a time; spx_ctx_set_group)"""
         _check(lib().spx_ctx_set_group(self.h, int(k)))
-
-    def set_msm_pairing(self, us):
-        """merge this context's MSM batches with other contexts' identical batches, waiting up to `us`
-        microseconds for a partner (0 = never; spx_ctx_set_msm_pairing)"""
-        if not hasattr(lib(), "spx_ctx_set_msm_pairing") and not us:  # an A/B build that predates it
-            return
-        _check(lib().spx_ctx_set_msm_pairing(self.h, int(us)))
-
-    def msm_pairing_stats(self):
-        """(batches merged as the second context, batches run alone after waiting)"""
-        if not hasattr(lib(), "spx_ctx_msm_pairing_stats"):
-            return 0, 0
-        out = (ctypes.c_uint64 * 2)()
-        _check(lib().spx_ctx_msm_pairing_stats(self.h, out))
-        return out[0], out[1]
 
     def mem_info(self):
         """(free, total) bytes of this context's device (spx_ctx_mem_info)"""

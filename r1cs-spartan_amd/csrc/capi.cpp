@@ -664,20 +664,6 @@ int spx_ctx_set_sync_poll(spx_ctx* ctx, int us) {
         ctx->c->poll_us = us < 0 ? -1 : us;
     });
 }
-int spx_ctx_set_msm_pairing(spx_ctx* ctx, int us) {
-    return guard([&] {
-        if (!ctx) spx::invalid("null context");
-        if (ctx->c->in_use.load()) spx::invalid("context in use by a prove or session");
-        ctx->c->pair_us = us < 0 ? 0 : us;
-    });
-}
-int spx_ctx_msm_pairing_stats(spx_ctx* ctx, uint64_t out[2]) {
-    return guard([&] {
-        if (!ctx || !out) spx::invalid("null argument");
-        out[0] = ctx->c->msm_merged.load();
-        out[1] = ctx->c->msm_alone.load();
-    });
-}
 int spx_ctx_set_group(spx_ctx* ctx, int k) {
     return guard([&] {
         if (!ctx) spx::invalid("null context");

@@ -256,11 +256,6 @@ void launch_open_tail(const Fr* rin, Fr* q, uint64_t half, int nlev, const Fr* p
 struct MsmInst {
     uint64_t pts_off;     // first precomputed point of this base set
     uint64_t scalar_off;  // first scalar (Montgomery Fr) in the batch scalar array
-    const Fr* sc;         // the instance's scalars: null = scalars + scalar_off of the batch's array
-                          // (a batch merging two proofs' MSMs gives each instance its own pointer)
-    uint32_t own1;        // 1 + the instance's index in its own proof's list (an unsplit instance's
-                          // owner rank = that index mod world, the same however batches are merged);
-                          // 0 = its index in this batch
     uint32_t size;        // number of (base, scalar) pairs
     uint32_t c, W;        // window bits, windows
     uint32_t stride;      // points per window copy of the base set (>= size)

@@ -80,7 +80,7 @@ DEV bool scalar_keys(const MsmInst* __restrict__ insts, const uint64_t* __restri
     const uint64_t j = g - prefix[i];
     const MsmInst I = insts[i];
     Fr m, sc;
-    load_vec(m, I.sc + j);
+    load_vec(m, scalars + I.scalar_off + j);
     fe_from_mont(sc, m);
     Digits d;
 #pragma unroll
@@ -529,7 +529,7 @@ MsmPlan msm_plan(const MsmInst* ih, int ninst, const MsmShard& sh, double cap_sc
             I.sel = (uint32_t)sh.rank;
             split_refs += (double)I.size * I.W / G;
             ++nsplit;
-        } else if ((I.own1 ? I.own1 - 1 : (uint32_t)i) % G == (uint32_t)sh.rank) {  // whole, on its owner
+        } else if (i % G == sh.rank) {  // whole, on its owner
             I.lb = lbf;
             I.lg = 0;
             I.sel = 0;

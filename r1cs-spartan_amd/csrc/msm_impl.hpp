@@ -534,13 +534,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     const bool g2 = sizeof(F) == sizeof(Fq2);
     const size_t psz = sizeof(Xyzz<F>);
     const size_t ob = msm_out_bytes(g2, ninst);
-    std::vector<MsmInst> iv(ih, ih + ninst);  // every instance's own scalar pointer (MsmInst::sc)
-    for (auto& I : iv)
-        if (!I.sc) {
-            if (!scalars) throw std::runtime_error("MSM: instance without scalars");
-            I.sc = scalars + I.scalar_off;
-        }
-    MsmPlan pl = msm_plan(iv.data(), ninst, sh, ws->cap_scale);
+    MsmPlan pl = msm_plan(ih, ninst, sh, ws->cap_scale);
     const int nact = (int)pl.insts.size();
     if (!nact) {  // nothing of this batch is this rank's: every output is infinity (all zero), status 0
         HIPCHK(hipMemsetAsync(out_dev, 0, ob, s));

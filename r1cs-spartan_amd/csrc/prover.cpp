@@ -107,8 +107,6 @@ Ctx::~Ctx() {
     (void)hipSetDevice(device);
     if (msm_side) msm_ws_destroy(msm_side);
     if (side_ev) (void)hipEventDestroy(side_ev);
-    if (pair_ready) (void)hipEventDestroy(pair_ready);
-    if (pair_done) (void)hipEventDestroy(pair_done);
     if (side) (void)hipStreamDestroy(side);
     msm_ws_destroy(msm);
     scratch.release();
@@ -908,126 +906,6 @@ static std::vector<HFr> allgather_fr(Comm& comm, const std::vector<HFr>& mine) {
     return all;
 }
 
-// ---------------------------------------------------------------- MSM batches of two proofs merged
-// (spx_ctx_set_msm_pairing). A rank of a G-rank proof runs 1/G of each MSM: its accumulation grids
-// are one round of resident waves deep and every batch pays its own latency-bound tail (partial
-// levels, weighting tree, the sort's launches). When another context of this process reaches the
-// same batch of its own proof (same curve, kind, shape, public parameter and shard), the two batches
-// run as ONE on the context that arrives second: it waits on the host until the first one's scalars
-// are in place (an event), runs the merged instance list through the MSM pipeline once (grids twice
-// as deep, one tail for both) and copies each proof's outputs and the shared status words straight
-// into that proof's pinned host buffer; the first context's next sync also waits for the event the
-// second records after those copies. No stream ever waits on another stream's event: with more
-// streams than hardware queues such a wait blocks the queue for every stream mapped to it (measured:
-// a G = 8 rank fell from 418 to 240 M constraints/s with stream-side waits). Every instance keeps its
-// own scalars (MsmInst::sc) and its owner rank (MsmInst::own1), so every output is the one an
-// unmerged batch gives; an overflowed merged batch makes both proofs rerun theirs dense, alone. A
-// context that finds no partner within pair_us microseconds runs its batch alone.
-struct PairPost {
-    bool g2;
-    int kind, ninst, rank, world;
-    uint32_t size0;
-    const void* pts;
-    Ctx* C;
-    std::vector<MsmInst> insts;  // sc and own1 set
-    uint8_t* host;               // pinned destination of the outputs + status words
-    hipEvent_t ready, done;
-    bool taken = false, finished = false;
-    std::exception_ptr err;
-    bool matches(const PairPost& o) const {
-        return g2 == o.g2 && kind == o.kind && ninst == o.ninst && rank == o.rank && world == o.world &&
-               size0 == o.size0 && pts == o.pts && C != o.C;
-    }
-};
-static std::mutex g_pair_mu;
-static std::condition_variable g_pair_cv;
-static std::vector<PairPost*> g_pair_wait;
-enum { kPairCommit = 1, kPairLvl0, kPairOpen };
-
-static void msm_run_any(Ctx& C, bool g2, const MsmInst* insts, int n, const void* pts, const Fr* scalars, void* out,
-                        const MsmShard& sh) {
-    if (g2)
-        msm_run_g2(C.msm, insts, n, static_cast<const G2Aff*>(pts), scalars, out, C.stream, sh);
-    else
-        msm_run_g1(C.msm, insts, n, static_cast<const G1Slot*>(pts), scalars, out, C.stream, sh);
-}
-// One MSM batch of this proof on C.stream: outputs (msm_out_bytes) in `out` and copied to the pinned
-// `host` (ready after this context's next sync), merged with another context's identical batch when
-// possible (above).
-static void msm_batch(Ctx& C, bool g2, int kind, const MsmInst* insts, int n, const void* pts, const Fr* scalars, void* out,
-                      uint8_t* host, const MsmShard& sh) {
-    const size_t ob = msm_out_bytes(g2, n);
-    const int us = C.pair_us.load(std::memory_order_relaxed);
-    auto alone = [&](const MsmInst* in, const Fr* sc) {
-        msm_run_any(C, g2, in, n, pts, sc, out, sh);
-        SPX_HIP(hipMemcpyAsync(host, out, ob, hipMemcpyDeviceToHost, C.stream));
-    };
-    if (us <= 0 || sh.dense || n <= 0) {
-        alone(insts, scalars);
-        return;
-    }
-    PairPost me;
-    me.g2 = g2, me.kind = kind, me.ninst = n, me.rank = sh.rank, me.world = sh.world;
-    me.size0 = insts[0].size, me.pts = pts, me.C = &C, me.host = host;
-    me.insts.assign(insts, insts + n);
-    for (int i = 0; i < n; ++i) {
-        if (!me.insts[i].sc) me.insts[i].sc = scalars + me.insts[i].scalar_off;
-        me.insts[i].own1 = (uint32_t)i + 1;
-    }
-    C.ensure_pair_events();
-    me.ready = C.pair_ready, me.done = C.pair_done;
-    SPX_HIP(hipEventRecord(me.ready, C.stream));
-    PairPost* first = nullptr;
-    {
-        std::unique_lock<std::mutex> lk(g_pair_mu);
-        for (auto it = g_pair_wait.begin(); it != g_pair_wait.end(); ++it)
-            if ((*it)->matches(me)) {
-                first = *it;
-                g_pair_wait.erase(it);
-                first->taken = true;
-                break;
-            }
-        if (!first) {  // wait for a partner to take this batch
-            g_pair_wait.push_back(&me);
-            if (!g_pair_cv.wait_for(lk, std::chrono::microseconds(us), [&] { return me.taken; })) {
-                g_pair_wait.erase(std::find(g_pair_wait.begin(), g_pair_wait.end(), &me));
-                lk.unlock();
-                ++C.msm_alone;
-                alone(me.insts.data(), nullptr);
-                return;
-            }
-            g_pair_cv.wait(lk, [&] { return me.finished; });
-            if (me.err) std::rethrow_exception(me.err);
-            C.pair_pending = me.done;  // this context's next sync waits for the merged batch's copies
-            return;
-        }
-    }
-    // second to arrive: the merged batch on this context's stream and MSM workspace
-    try {
-        SPX_HIP(hipEventSynchronize(first->ready));  // the first proof's scalars are in place
-        std::vector<MsmInst> all(me.insts);
-        all.insert(all.end(), first->insts.begin(), first->insts.end());
-        const size_t rb = (g2 ? 4 * 96 : 4 * 48) * (size_t)n;
-        uint8_t* mo = C.buf<uint8_t>(Ctx::kSlotPairOut, msm_out_bytes(g2, 2 * n));
-        msm_run_any(C, g2, all.data(), 2 * n, pts, nullptr, mo, sh);
-        SPX_HIP(hipMemcpyAsync(host, mo, rb, hipMemcpyDeviceToHost, C.stream));
-        SPX_HIP(hipMemcpyAsync(host + rb, mo + 2 * rb, 16, hipMemcpyDeviceToHost, C.stream));
-        SPX_HIP(hipMemcpyAsync(first->host, mo + rb, rb, hipMemcpyDeviceToHost, C.stream));
-        SPX_HIP(hipMemcpyAsync(first->host + rb, mo + 2 * rb, 16, hipMemcpyDeviceToHost, C.stream));
-        SPX_HIP(hipEventRecord(first->done, C.stream));
-        ++C.msm_merged;
-    } catch (...) {
-        std::lock_guard<std::mutex> lk(g_pair_mu);
-        first->err = std::current_exception();
-        first->finished = true;
-        g_pair_cv.notify_all();
-        throw;
-    }
-    std::lock_guard<std::mutex> lk(g_pair_mu);
-    first->finished = true;
-    g_pair_cv.notify_all();
-}
-
 // ---------------------------------------------------------------- commit (commit.rs:17-29)
 // Split in two so the MSM runs while the host absorbs the matrices into the transcript: launch
 // enqueues the MSM and the copy of its XYZZ result into pinned memory; finish waits and decodes.
@@ -1042,7 +920,8 @@ static void commit_launch(Ctx& C, PP& P, const Fr* z, uint64_t n, const MsmShard
     inst.W = (uint32_t)P.g1_W;
     const size_t ob = msm_out_bytes(false, 1);
     void* out = C.buf(Ctx::kSlotCommit, ob);
-    msm_batch(C, false, kPairCommit, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, C.pin_at(Ctx::kPinCommit, ob, 4 << 10), sh);
+    msm_run_g1(C.msm, &inst, 1, P.g1_pre.as<G1Slot>(), z, out, C.stream, sh);
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinCommit, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, C.stream));
 }
 static Affine<HFq> commit_finish(Ctx& C, PP& P, const Fr* z, uint64_t n, Comm& comm) {
     C.sync();
@@ -1091,12 +970,8 @@ static void lvl0_launch(Ctx& C, PP& P, const Fr* z, int L, const MsmShard& sh, b
     I.W = (uint32_t)P.g2_W[0];
     const size_t ob = msm_out_bytes(true, 1);
     void* out = C.buf(Ctx::kSlotLvl0Out, ob);
-    if (on_side) {
-        msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
-        SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
-    } else {
-        msm_batch(C, true, kPairLvl0, &I, 1, P.g2_pre.as<G2Aff>(), q, out, C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), sh);
-    }
+    msm_run_g2(ws, &I, 1, P.g2_pre.as<G2Aff>(), q, out, st, sh);
+    SPX_HIP(hipMemcpyAsync(C.pin_at(Ctx::kPinLvl0, ob, 4 << 10), out, ob, hipMemcpyDeviceToHost, st));
 }
 static Affine<HFq2> lvl0_finish(Ctx& C, PP& P, const Fr* z, int L, Comm& comm, bool on_side = false) {
     if (on_side)
@@ -1193,7 +1068,8 @@ static OpenOut open_z(Ctx& C, PP& P, const Fr* z, int L, const std::vector<HFr>&
         MsmShard sh = shard_of(comm);
         sh.dense = attempt > 0;
         if (nm) {
-            msm_batch(C, true, kPairOpen, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, h, sh);
+            msm_run_g2(C.msm, insts.data(), nm, P.g2_pre.as<G2Aff>(), q, out, C.stream, sh);
+            SPX_HIP(hipMemcpyAsync(h, out, ob, hipMemcpyDeviceToHost, C.stream));
         }
         if (!attempt) SPX_HIP(hipMemcpyAsync(h + ob, rin, 32, hipMemcpyDeviceToHost, C.stream));
         C.sync();
@@ -1296,10 +1172,6 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
             if (std::uncaught_exceptions() <= pending) return;
             (void)hipStreamSynchronize(C.stream);
             if (C.side) (void)hipStreamSynchronize(C.side);
-            if (C.pair_pending) {  // a merged MSM batch may still read this proof's scalars
-                (void)hipEventSynchronize(C.pair_pending);
-                C.pair_pending = nullptr;
-            }
             msm_ws_staging_reset(C.msm);
             if (C.msm_side) msm_ws_staging_reset(C.msm_side);
         }

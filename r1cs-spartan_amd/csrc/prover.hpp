@@ -195,7 +195,7 @@ struct Ctx {
     // per-prove scratch (grow-only: no hipMalloc/hipFree, which synchronise the device, while proofs
     // on other contexts are in flight)
     DevMem scratch;
-    enum { kSlotCommit, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlotPairOut, kSlots };
+    enum { kSlotCommit, kSlotOpenQ, kSlotOpenA, kSlotOpenB, kSlotOpenOut, kSlotLvl0Q, kSlotLvl0Out, kSlots };
     DevMem slot[kSlots];
     template <class T = void>
     T* buf(int id, size_t bytes) {
@@ -227,26 +227,9 @@ struct Ctx {
     // spx_prove_many on this context proves its stubbed-commitment, unsharded proofs in lockstep groups
     // of this many (prove_group; 1 = one at a time)
     std::atomic<int> group{1};
-    // MSM batches merged with another context's identical batch (prover.cpp msm_batch): wait up to
-    // this many microseconds for a partner (0 = never merge); the batches merged (as the second
-    // context) and run alone after waiting
-    std::atomic<int> pair_us{0};
-    std::atomic<uint64_t> msm_merged{0}, msm_alone{0};
-    hipEvent_t pair_ready = nullptr, pair_done = nullptr;
-    // set when this context's last MSM batch ran merged on another context: the event recorded there
-    // after this proof's outputs reached its pinned buffer (sync() waits for it)
-    hipEvent_t pair_pending = nullptr;
-    void ensure_pair_events() {
-        if (!pair_ready) SPX_HIP(hipEventCreateWithFlags(&pair_ready, hipEventDisableTiming));
-        if (!pair_done) SPX_HIP(hipEventCreateWithFlags(&pair_done, hipEventDisableTiming));
-    }
     void wait_stream(hipStream_t s);
     void sync() {  // the main stream's work is done: its MSM staging may be reused
         wait_stream(stream);
-        if (pair_pending) {  // and a merged MSM batch that carried this proof's instances
-            SPX_HIP(hipEventSynchronize(pair_pending));
-            pair_pending = nullptr;
-        }
         msm_ws_staging_reset(msm);
         if (kprof.on) kprof.harvest();
     }

@@ -39,9 +39,6 @@ def main():
                     "slowest rank, so node_estimate = the minimum over them")
     ap.add_argument("--exchange-ns", type=int, default=0,
                     help="--solo: charge every exchange this latency (SPX_REHEARSAL_EXCHANGE_NS; 0 = free)")
-    ap.add_argument("--pair-us", type=int, default=-1,
-                    help="merge MSM batches of two contexts' proofs, waiting up to this many us for a partner "
-                    "(spx_ctx_set_msm_pairing; 0 = off; default: bench.pair_us_for(G))")
     ap.add_argument("--exchange-list", default="",
                     help="--solo: after the ranks, the slowest one again with every exchange charged each of these "
                     "latencies (ns, comma-separated)")
@@ -63,7 +60,6 @@ def main():
     for r in range(G):
         for k in range(B):
             ctxs[r][k].set_lvl0_batch(bench.lvl0_for(world) if a.lvl0 == -2 else a.lvl0)
-            ctxs[r][k].set_msm_pairing(bench.pair_us_for(world) if a.pair_us < 0 else a.pair_us)
             if a.solo:
                 ctxs[r][k].set_comm_rehearsal(solo_ranks[0], world)
             elif G > 1:
@@ -173,8 +169,6 @@ def main():
                       "node_spread": round(max(per_rank.values()) / node, 4) if per_rank else None,
                       "distinct": len(set(proofs)),
                       "msm_reruns": sum(c.msm_reruns() for cs in ctxs for c in cs), "device_memory": mem,
-                      "msm_batches_merged": sum(c.msm_pairing_stats()[0] for cs in ctxs for c in cs),
-                      "msm_batches_alone_after_wait": sum(c.msm_pairing_stats()[1] for cs in ctxs for c in cs),
                       "process_cores_busy": round(cpu / el, 2),
                       "process_cpu_ms_per_proof": round(cpu / npf * 1e3, 3),
                       # per proof, on the proving threads (prove()'s phases), excluding the hashing pool

@@ -527,6 +527,15 @@ __global__ __launch_bounds__(kTopThreads, 1) void k_tree_top(const MsmInst* __re
     }
 }
 
+// SPX_MSM_LEVELS=k (A/B): at most k XYZZ partial levels; the weighting leaf adds the rest
+static int msm_levels_env() {
+    static const int v = [] {
+        const char* e = getenv("SPX_MSM_LEVELS");
+        return e ? atoi(e) : -1;
+    }();
+    return v;
+}
+
 template <class F>
 static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const typename Acc<F>::Pt* pts, const Fr* scalars,
                       void* out_dev, hipStream_t s, const MsmShard& sh) {
@@ -552,6 +561,7 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     int nlev = 0;
     for (uint32_t m = (uint32_t)std::ceil((mu + 6.0 * std::sqrt(mu) + 16.0) / kSeg1) + 1; m > 1; m = (m + kSeg - 1) / kSeg)
         ++nlev;  // partials per bucket, divided by kSeg per level
+    if (msm_levels_env() >= 0) nlev = std::min(nlev, msm_levels_env());
     // the sort's first launch zeroes the outputs (infinity) and the status words
     MsmSorted so = msm_sort(ws, pl, scalars, out_dev, ob, s, kSeg1, nlev);
     const uint64_t max_segs = tot_refs / kSeg1 + nb + 1;

@@ -535,6 +535,14 @@ static int msm_levels_env() {
     }();
     return v;
 }
+// SPX_MSM_SEG1=k (A/B): at most k references per accumulation thread
+static int msm_seg1_env() {
+    static const int v = [] {
+        const char* e = getenv("SPX_MSM_SEG1");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
 
 template <class F>
 static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const typename Acc<F>::Pt* pts, const Fr* scalars,
@@ -553,7 +561,8 @@ static void msm_run_t(MsmWorkspace* ws, const MsmInst* ih, int ninst, const type
     const uint32_t nb = pl.nb;
     const uint64_t tot_refs = pl.tot_refs;
     // level 1: affine references -> XYZZ partials, one per segment of kSeg1 references
-    const uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
+    uint32_t kSeg1 = seg1_fit(seg1_len(g2), tot_refs, Acc<F>::kWaves, Acc<F>::kLanes);
+    if (msm_seg1_env() > 0) kSeg1 = std::min<uint32_t>(kSeg1, (uint32_t)msm_seg1_env());
     // XYZZ partial levels, planned from the expected occupancy (no host round trip): a bucket with
     // mu references on average rarely exceeds mu + 6 sqrt(mu) + 16; the weighting leaf adds the
     // partials of any bucket that does (k_tree_chunk), so the plan decides speed, never correctness

@@ -418,8 +418,8 @@ def largest_rate(d):
 # sumcheck rounds grouped (more queues: lower; profiles/r05/r05zh_c2group.jsonl, r05zi_c2group.jsonl),
 # 2,114 - 2,190 M with every step grouped (r05zl_c2group.jsonl; 64 / 128 / 192 / 256 in flight: 1,987 /
 # 2,142 - 2,165 / 2,114 - 2,122 / 2,137 - 2,190 M). C2_INFLIGHT counts proofs in flight.
-C2_INFLIGHT = 128
-C2_GROUP = 8
+C2_INFLIGHT = int(os.environ.get("SPX_BENCH_C2_INFLIGHT", "128"))
+C2_GROUP = int(os.environ.get("SPX_BENCH_C2_GROUP", "8"))  # (A/B: up to 16, spx_ctx_set_group's limit)
 C2_SYNC_POLL_US = 20
 
 

@@ -140,7 +140,7 @@ int spx_ctx_comm_allgather(spx_ctx *ctx, const void *send, void *recv, size_t by
  * with matrices absorbed per proof, sharded ranks), 0 = hipStreamSynchronize, -1 = the process default
  * (SPX_SYNC_POLL_US, else 0). */
 int spx_ctx_set_sync_poll(spx_ctx *ctx, int us);
-/* Lockstep groups for spx_prove_many (no effect on the proof bytes): with k > 1 (at most 8) the
+/* Lockstep groups for spx_prove_many (no effect on the proof bytes): with k > 1 (at most 16) the
  * context's stubbed-commitment proofs on an unsharded context (BASELINE C2) run k at a time in
  * lockstep: each sumcheck round of the k proofs is one launch (blockIdx.y = proof) with one host wait,
  * and the other steps queue the k proofs' launches before one wait. Other proofs, and

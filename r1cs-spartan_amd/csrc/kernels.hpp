@@ -70,7 +70,7 @@ struct Tables3 {
 // Lockstep groups (spx_ctx_set_group): one launch runs the same sumcheck round of up to kGroupMax
 // proofs of one index, proof j's blocks at blockIdx.y = j, each with its own tables, challenge,
 // partials, ticket and result (the per-proof launches' arguments, passed by value)
-static constexpr int kGroupMax = 8;
+static constexpr int kGroupMax = 16;
 // the last rounds of each sumcheck a lockstep group runs on the host (prove_group): <= 5 (the tables
 // then fit each proof's 8 KiB pinned region)
 static constexpr int kGroupHostTail = 5;

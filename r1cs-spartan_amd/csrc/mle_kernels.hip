@@ -1187,9 +1187,9 @@ __global__ __launch_bounds__(kTailMax) void k_open_tail(const Fr* __restrict__ r
 // = j with its own job (pointers, points), everything else shared. The bodies see blockIdx.x and
 // gridDim.x of their own proof, as in the per-proof launch (k_spmv_sliced's XCD eighths included: the
 // per-proof grid is a multiple of 8, so the linear workgroup id keeps blockIdx.x mod 8).
-template <class J>
+template <class J, int N = kGroupMax>
 struct GroupOf {
-    J j[kGroupMax];
+    J j[N];
 };
 struct SpmvJob {
     const Fr* z;
@@ -1304,10 +1304,17 @@ __global__ __launch_bounds__(kThreads) void k_open_level_group(GroupOf<LevelJob>
     const LevelJob& j = g.j[blockIdx.y];
     k_open_level_body(j.rin, j.rout, nullptr, j.p, half);
 }
-__global__ __launch_bounds__(kTailMax) void k_open_tail_group(GroupOf<TailJob> g, uint32_t h0, int nlev) {
+// (a tail job carries its points by value: 336 B, so a tail launch takes at most kTailGroup proofs and
+// its arguments stay below 4 KiB)
+static constexpr int kTailGroup = 8;
+__global__ __launch_bounds__(kTailMax) void k_open_tail_group(GroupOf<TailJob, kTailGroup> g, uint32_t h0, int nlev) {
     const TailJob& j = g.j[blockIdx.y];
     k_open_tail_body(j.rin, nullptr, h0, nlev, j.pts, j.last);
 }
+static_assert(sizeof(GroupOf<TailJob, kTailGroup>) <= 4096 && sizeof(GroupOf<FoldJob<3>>) <= 4096 &&
+                  sizeof(GroupOf<ColJob>) <= 4096 && sizeof(GroupOf<EqfJob>) <= 4096 && sizeof(Sc1Group) <= 4096 &&
+                  sizeof(Sc2Group) <= 4096,
+              "a group launch's arguments stay below 4 KiB");
 // proof blockIdx.x: n runs of `per` Fr (src[i][0 .. per)) -> dst[per i ..] (host-mapped pinned memory:
 // a group's small device-to-host results in one launch instead of a copy per run)
 __global__ void k_copy_runs_group(GroupOf<CopyJob> g, int n, int per) {
@@ -1654,13 +1661,16 @@ void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* cons
         Fr* const* rout = (nb++ & 1) ? bufB : bufA;
         const uint64_t half = n >> (i + 1);
         if (open_tail_levels(half, L - i) == L - i) {  // the remaining levels, straight into `last`
-            GroupOf<TailJob> g{};
-            for (int j = 0; j < k; ++j) {
-                g.j[j].rin = rin[j];
-                g.j[j].last = last[j];
-                for (int q = i; q < L; ++q) g.j[j].pts.p[q - i] = points[(size_t)j * L + q];
+            for (int j0 = 0; j0 < k; j0 += kTailGroup) {
+                const int kk = std::min(kTailGroup, k - j0);
+                GroupOf<TailJob, kTailGroup> g{};
+                for (int j = 0; j < kk; ++j) {
+                    g.j[j].rin = rin[j0 + j];
+                    g.j[j].last = last[j0 + j];
+                    for (int q = i; q < L; ++q) g.j[j].pts.p[q - i] = points[(size_t)(j0 + j) * L + q];
+                }
+                hipLaunchKernelGGL(k_open_tail_group, dim3(1, kk), dim3(kTailMax), 0, s, g, (uint32_t)half, L - i);
             }
-            hipLaunchKernelGGL(k_open_tail_group, dim3(1, k), dim3(kTailMax), 0, s, g, (uint32_t)half, L - i);
             tail = true;
             break;
         }

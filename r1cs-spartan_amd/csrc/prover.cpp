@@ -1655,11 +1655,11 @@ std::vector<std::vector<uint8_t>> prove_group(Ctx& C, Index& I, Witness* const* 
     // the group's challenges: proof j's tau, r_x, r_abc at chg + 8 L j (one host-to-device copy each time)
     C.scratch.ensure(32 * (need + 8 * (uint64_t)L) * (uint64_t)k);
     Fr* chg = C.scratch.as<Fr>() + need * k;
-    static_assert(kGroupMax * 8192 <= (64 << 10), "per-proof pinned regions");
-    if (32 * (L + 3) > 4096 || 32 * 8 * L * kGroupMax > (64 << 10)) invalid("log_n too large for a lockstep group");
-    uint8_t* hp0 = C.pin_at(Ctx::kPinHp, kGroupMax * 8192, 64 << 10);
+    static_assert(kGroupMax * 8192 <= (128 << 10), "per-proof pinned regions");
+    if (32 * (L + 3) > 4096 || 32 * 8 * L * kGroupMax > (128 << 10)) invalid("log_n too large for a lockstep group");
+    uint8_t* hp0 = C.pin_at(Ctx::kPinHp, kGroupMax * 8192, 128 << 10);
     uint8_t* ho0 = C.pin_at(Ctx::kPinOpen, kGroupMax * 2048, 56 << 10);
-    uint8_t* stage = C.pin_at(Ctx::kPinStage, (size_t)32 * 8 * L * k, 64 << 10);
+    uint8_t* stage = C.pin_at(Ctx::kPinStage, (size_t)32 * 8 * L * k, 128 << 10);
     struct P {
         Fr *Az, *Bz, *Cz, *F1[3], *F2[3], *E1, *Ea, *Eb, *M0, *M1, *M2, *Z1, *Z2, *partial, *eqlo, *eqhi, *eqf, *chdev;
         Fr *oA, *oB;

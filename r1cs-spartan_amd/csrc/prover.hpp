@@ -178,12 +178,12 @@ struct Ctx {
     // caller holds stays valid while its async copies run). Every region is reused only after a
     // stream sync that covers the copies issued from it.
     enum : size_t {
-        kPinHp = 0,                 // prove(): challenges up, round results down (64 KiB)
-        kPinCommit = 64 << 10,      // commitment MSM result + status (4 KiB)
-        kPinLvl0 = 68 << 10,        // shared level-0 opening proof + status (4 KiB)
-        kPinOpen = 72 << 10,        // opening results + status / evaluations (56 KiB)
-        kPinStage = 128 << 10,      // small host-to-device staging (opening points, constants) (64 KiB)
-        kPinBytes = 192 << 10
+        kPinHp = 0,                 // prove(): challenges up, round results down (128 KiB: 8 KiB per proof of a group)
+        kPinCommit = 128 << 10,     // commitment MSM result + status (4 KiB)
+        kPinLvl0 = 132 << 10,       // shared level-0 opening proof + status (4 KiB)
+        kPinOpen = 136 << 10,       // opening results + status / evaluations (56 KiB)
+        kPinStage = 192 << 10,      // small host-to-device staging (opening points, constants, a group's challenges) (128 KiB)
+        kPinBytes = 320 << 10
     };
     uint8_t* pin = nullptr;
     uint8_t* pin_dev_base = nullptr;  // the carve-out's device address (kernels write round results there)

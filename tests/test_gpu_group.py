@@ -29,7 +29,7 @@ def test_group_equals_single(spx, ctx, oc, log_n, mode):
     log_v = 3
     syn, pk, wits = _instance(spx, ctx, log_n, log_v, 7)
     want = [spx.MLArgumentForR1CS.prove_witness(pk, w, None, mode=mode, seed=5, commitment_stub=True) for w in wits]
-    for k in (2, 3, 8):
+    for k in (2, 3, 8, 16):
         ctxs = [spx.Context(0) for _ in range(2)]
         for c in ctxs:
             c.set_group(k)
@@ -45,12 +45,15 @@ def test_group_equals_single(spx, ctx, oc, log_n, mode):
 
 @pytest.mark.gpu
 def test_group_c2_size(spx, ctx):
-    """BASELINE C2's size, 2^18: a group of 8 and a ragged group of 3 against one-at-a-time proofs"""
+    """BASELINE C2's size, 2^18: a group of 8 and a ragged group of 3, then one group of 11 (group size
+    16), against one-at-a-time proofs"""
     log_n, log_v = 18, 5
     syn, pk, wits = _instance(spx, ctx, log_n, log_v, 11)
     want = [spx.MLArgumentForR1CS.prove_witness(pk, w, None, cached=True, commitment_stub=True) for w in wits]
     c = spx.Context(0)
     c.set_group(8)
+    assert spx.MLArgumentForR1CS.prove_many([c], pk, wits, None, cached=True, commitment_stub=True) == want
+    c.set_group(16)  # one group of 11: more than one tail launch's 8 proofs
     assert spx.MLArgumentForR1CS.prove_many([c], pk, wits, None, cached=True, commitment_stub=True) == want
 
 
@@ -69,7 +72,7 @@ def test_group_leaves_full_proofs_alone(spx, ctx, oc):
 @pytest.mark.gpu
 def test_group_size_checked(spx, ctx):
     c = spx.Context(0)
-    for bad in (0, 9, -1):
+    for bad in (0, 17, -1):
         with pytest.raises(spx.InvalidArgument):
             c.set_group(bad)
     c.set_group(1)

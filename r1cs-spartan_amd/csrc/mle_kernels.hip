@@ -14,7 +14,6 @@
 #include "kernels.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 #include <vector>
 #include <stdexcept>
@@ -1287,55 +1286,6 @@ __global__ __launch_bounds__(kThreads) void k_eq_expand_group(GroupOf<EqxJob> g,
     const EqxJob& j = g.j[blockIdx.y];
     k_eq_expand_body(j.lo, j.hi, klo, base, count, j.out);
 }
-// Two proofs of the group per block (blockIdx.y = pair): each entry's (row | matrix, value) is loaded
-// once for both, and the two proofs' factor gathers and products are independent chains. Same products
-// and the same summation order per proof as k_col_stream_body, so the same bytes.
-__global__ __launch_bounds__(kThreads) void k_col_stream_group2(ColStreamView cv, GroupOf<ColJob> g, int k) {
-    const int p0 = 2 * blockIdx.y, p1 = p0 + 1 < k ? p0 + 1 : p0;
-    const ColJob& J0 = g.j[p0];
-    const ColJob& J1 = g.j[p1];
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const Fr* __restrict__ lo0 = J0.ef.t[0];
-    const Fr* __restrict__ hi0 = J0.ef.t[1];
-    const Fr* __restrict__ lo1 = J1.ef.t[0];
-    const Fr* __restrict__ hi1 = J1.ef.t[1];
-    const int klo = J0.ef.k[0], khi = J0.ef.k[1];
-    const uint32_t mask = (1u << klo) - 1;
-    auto hidx = [&](uint32_t rm) { return ((rm >> 30) << khi) | ((rm & 0x3FFFFFFFu) >> klo); };
-    for (uint32_t w = wid; w < kColWindow; w += kThreads / 64) {
-        const uint32_t si = blockIdx.x * kColWindow + w;
-        if (si >= cv.nslices) break;
-        const ColSlice sl = cv.slices[si];
-        const uint32_t info = cv.lanes[(size_t)si * 64 + lane];
-        const uint32_t len = info == kColNone ? 0u : info >> 26;
-        Fr acc0, acc1;
-        fe_zero(acc0);
-        fe_zero(acc1);
-        const uint32_t* rp = cv.rowm + sl.off + lane;
-        const Fr* vp = cv.val + sl.off + lane;
-        for (uint32_t j = 0; j < len; ++j) {
-            const uint32_t r = rp[(size_t)j * 64];
-            const Fr v = ld_fr(vp + (size_t)j * 64);
-            const uint32_t il = r & mask, ih = hidx(r);
-            Fr a0 = ld_fr(lo0 + il), a1 = ld_fr(lo1 + il), b0 = ld_fr(hi0 + ih), b1 = ld_fr(hi1 + ih), t0, t1;
-            fr_mul_pair(t0, v, a0, t1, v, a1);
-            fr_mul_pair(t0, t0, b0, t1, t1, b1);
-            fe_add(acc0, acc0, t0);
-            fe_add(acc1, acc1, t1);
-        }
-        if (info != kColNone) {
-            st_fr(J0.out + (info & 0x3FFFFFFu), acc0);
-            if (p1 != p0) st_fr(J1.out + (info & 0x3FFFFFFu), acc1);
-        }
-    }
-}
-static int col_group2_env() {  // SPX_COL_GROUP2=0 (A/B): one proof per block
-    static const int v = [] {
-        const char* e = getenv("SPX_COL_GROUP2");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
 __global__ __launch_bounds__(kThreads) void k_col_stream_group(ColStreamView cv, GroupOf<ColJob> g) {
     const ColJob& j = g.j[blockIdx.y];
     k_col_stream_body(cv, j.ef, j.out);
@@ -1697,10 +1647,7 @@ void launch_col_stream_group(int k, const ColStreamView& cv, const Fr* const* r_
     hipLaunchKernelGGL(k_eq_factors_group, dim3(nf, k), dim3(kEqThreads), 0, s, gf);
     if (cv.nslices) {
         const uint32_t nwin = (cv.nslices + kColWindow - 1) / kColWindow;
-        if (col_group2_env() && k > 1)
-            hipLaunchKernelGGL(k_col_stream_group2, dim3(nwin, (k + 1) / 2), dim3(kThreads), 0, s, cv, gc, k);
-        else
-            hipLaunchKernelGGL(k_col_stream_group, dim3(nwin, k), dim3(kThreads), 0, s, cv, gc);
+        hipLaunchKernelGGL(k_col_stream_group, dim3(nwin, k), dim3(kThreads), 0, s, cv, gc);
     }
 }
 void launch_open_eval_group(int k, const Fr* const* z, Fr* const* bufA, Fr* const* bufB, const Fr* points, int L,

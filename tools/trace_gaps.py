@@ -35,3 +35,9 @@ for r in rows:
         by.setdefault(g, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for g, v in sorted(by.items(), key=lambda x: -len(x[1])):
     print("grid %s: %d launches, mean %.1f us, min %.1f, max %.1f" % (g, len(v), statistics.mean(v), min(v), max(v)))
+
+acc = [r for r in rows if "k_accum_aff<spx::Fq2>" in r["Kernel_Name"]]
+d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in acc]
+for lo in range(0, len(d), 30):
+    seg = d[lo : lo + 30]
+    print("launches %3d-%3d (time order): mean %.1f us" % (lo, lo + len(seg) - 1, statistics.mean(seg)))

@@ -41,3 +41,4 @@ d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in acc]
 for lo in range(0, len(d), 30):
     seg = d[lo : lo + 30]
     print("launches %3d-%3d (time order): mean %.1f us" % (lo, lo + len(seg) - 1, statistics.mean(seg)))
+print("last 9 launches (us):", " ".join("%.0f" % x for x in d[-9:]))

@@ -1259,7 +1259,10 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
         const char* e = getenv("SPX_LVL0");
         return e && std::string(e) == "batch";
     }();
-    const bool lvl0_batch = C.lvl0_mode >= 0 ? C.lvl0_mode == 1 : lvl0_batch_env;
+    // Unsharded index-cached proofs default to the batch form: with no absorption to hide level 0
+    // behind, one MSM pipeline less measured +2% index-cached at N = 1 (profiles/r06/r06zq_ab_lvl0_n1.jsonl)
+    const bool lvl0_batch =
+        C.lvl0_mode >= 0 ? C.lvl0_mode == 1 : (lvl0_batch_env || (G == 1 && o.cached && I.has_cache && !o.coins));
     // SPX_CHECK_DERIVED=1 (tests): from round 2 on, a sumcheck round's value at 1 is derived from the
     // previous claim on the host (P(0) + P(1) = claim); with this set the device computes it too and the
     // prove fails with SPX_SUMCHECK if they differ (the identity pinned round by round, every rank count)

@@ -1250,8 +1250,9 @@ std::vector<uint8_t> prove(Ctx& C, Index& I, Witness& W, PP* P, const ProveOpts&
     }
     // The shared level-0 opening proof is launched right behind the commitment, before any challenge,
     // when the host has the matrix absorption to do meanwhile. With the index-cached transcript there
-    // is nothing to hide it behind: it then runs on the context's second stream, beside the commitment
-    // and the first opening, and is reused by the second opening. (Both forms give every rank the same
+    // is nothing to hide it behind: a sharded proof then runs it on the context's second stream, beside
+    // the commitment and the first opening (reused by the second opening); an unsharded one puts it in
+    // the first opening's batch (below). (Both forms give every rank the same
     // batches, so the exchanges of a proof-sharded prove line up.)
     // SPX_LVL0=batch (A/B; must be the same on every rank of a proof-sharded prove): level 0 inside the
     // first opening's MSM batch instead, one MSM pipeline (sort, weighting tree) less per proof
